@@ -1,0 +1,39 @@
+# Build libqhuff.so (product: HIP kernels for gfx950 + C drop-ins) and the
+# oracle's CPU library (test infrastructure).  Used by __graft_entry__.build().
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+CSRC    := nghttp3_amd/csrc
+LIBDIR  := nghttp3_amd/lib
+LIB     := $(LIBDIR)/libqhuff.so
+ORACLE  := oracle/libqh_oracle.so
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
+            -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+CFLAGS   := -std=c11 -O2 -fPIC -fvisibility=hidden -Wall -Wextra
+
+all: $(LIB) $(ORACLE)
+
+$(CSRC)/qh_tables.h: nghttp3_amd/tools/gen_tables.py
+	python3 nghttp3_amd/tools/gen_tables.py $@
+
+$(LIBDIR)/qh_scalar.o: $(CSRC)/qh_scalar.c $(CSRC)/qh_tables.h include/qhuff.h
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/qh_tables.h include/qhuff.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# Oracle: -O2 -mavx2 as nghttp3's README.rst:61-67 prescribes for the
+# reference build (the Huffman loop itself has no SIMD path).
+$(ORACLE): oracle/qh_oracle.c oracle/qh_oracle.h
+	$(CC) -std=c11 -O2 -mavx2 -fPIC -shared -pthread -Wall -o $@ $<
+
+clean:
+	rm -f $(LIBDIR)/*.o $(LIB) $(ORACLE)
+
+.PHONY: all clean

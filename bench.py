@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: "GiB/s device-resident QPACK Huffman
+encode+decode, 1M strings; bit-exact".
+
+One step = one round trip of the hot path over one batch that is already
+resident in HBM: qh_encode_batch (encode_count -> scan -> encode) of 2^20
+synthetic header strings (8-256 B, alphabet A, BASELINE config 3 shape, seed
+0x5EED0003) followed by qh_decode_batch (slot scan -> decode) of the encoded
+strings.  value = plaintext bytes of all ranks x steps / max-over-ranks wall
+time, in GiB/s.  The decoded output is checked against the input after the
+timed region (bit-exact), and per-kernel HIP-event times from a second pass
+give the roofline of the dominant kernel.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank encodes and
+decodes its own independent batch (weak scaling, no data-path collective);
+RCCL is used only for the barrier and the max/sum reductions of the report.
+
+CPU baseline (rank 0, N = 1): the oracle restatement of
+lib/nghttp3_qpack_huffman.c (oracle/, -O2 -mavx2) round-trips the same
+strings on T host threads.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1 << 20, help="strings per GPU")
+    ap.add_argument("--lo", type=int, default=8)
+    ap.add_argument("--hi", type=int, default=256)
+    ap.add_argument("--alphabet", choices=["A", "U"], default="A")
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0003)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-reps", type=int, default=6)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="just run warmup+steps (for rocprofv3), minimal reporting")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    from nghttp3_amd import HuffmanBatchCodec, synth
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def reduce(x, op):
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    codec = HuffmanBatchCodec(device=local_rank)  # on torch's current stream
+    alphabet = synth.ALPHABET_A if args.alphabet == "A" else synth.ALPHABET_U
+    seed = args.seed + rank  # rank 0 keeps the config seed (digests in tests/golden)
+    n = args.n
+    src, spans, total = codec.synth(seed, n, args.lo, args.hi, alphabet)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc_bound = int(((ln * 30 + 7) // 8).sum().item())
+    enc = torch.empty(max(enc_bound, 1), dtype=torch.uint8, device=dev)
+    eout = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    dout = torch.empty((n, 2), dtype=torch.int64, device=dev)
+
+    # size the decode destination from the real encoded lengths (slot layout)
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    elen = eout[:, 1] & 0xFFFFFFFF
+    enc_bytes = int(elen.sum().item())
+    dec_cap = int(((elen * 8) // 5).sum().item())
+    dec = torch.empty(max(dec_cap, 1), dtype=torch.uint8, device=dev)
+
+    def step():
+        codec.encode_dev(src, spans, enc, eout)
+        codec.decode_dev(enc, eout, dec, dout)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = reduce(elapsed, dist.ReduceOp.MAX if world > 1 else None)
+
+    if args.profile_only:
+        if rank == 0:
+            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed_max / args.steps}))
+        return
+
+    # ---- bit-exact check of the last step (outside the timed region) ----
+    dstat = dout[:, 1] >> 32
+    dlen = dout[:, 1] & 0xFFFFFFFF
+    ok = bool((dstat == 0).all()) and bool((dlen == ln).all())
+    if ok:
+        rep_d = torch.repeat_interleave(dout[:, 0], ln)
+        rep_p = torch.repeat_interleave(spans[:, 0], ln)
+        pos = torch.arange(total, device=dev, dtype=torch.int64) - rep_p
+        ok = bool((dec[rep_d + pos] == src[:total]).all())
+        del rep_d, rep_p, pos
+    bad = reduce(0.0 if ok else 1.0, dist.ReduceOp.SUM if world > 1 else None)
+
+    # ---- per-kernel HIP-event times over a second timed pass ----
+    codec.enable_timing(True)
+    for _ in range(args.steps):
+        step()
+    ktimes = codec.kernel_times()
+    codec.enable_timing(False)
+
+    # decode-only / encode-only pipeline rates (wall clock, this rank)
+    def timed(fn, reps):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps
+
+    t_dec = timed(lambda: codec.decode_dev(enc, eout, dec, dout), args.steps)
+    t_enc = timed(lambda: codec.encode_dev(src, spans, enc, eout), args.steps)
+
+    total_all = reduce(float(total), dist.ReduceOp.SUM if world > 1 else None)
+    value = total_all * args.steps / elapsed_max / GIB
+
+    # roofline: dominant kernel by time; algorithmic bytes per launch
+    algo = {
+        "qh_k_decode": enc_bytes + total + 32 * n,       # E + D + 16 B in + 16 B out span
+        "qh_k_encode": total + enc_bytes + 32 * n,       # D + E + spans
+        "qh_k_count": total + 16 * n + 8 * n,            # D + in span + out len/status
+        "qh_k_scan_slots": 16 * n + 8 * n,
+        "qh_k_scan_hlen": 16 * n + 8 * n,
+    }
+    kern = {}
+    for name, (cnt, ms) in ktimes.items():
+        avg_ms = ms / max(cnt, 1)
+        gbps = algo.get(name, 0) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        kern[name] = {"launches": cnt, "avg_us": round(avg_ms * 1e3, 2),
+                      "algo_bytes": algo.get(name), "achieved_GBps": round(gbps, 1)}
+    dom = max(kern, key=lambda k: kern[k]["avg_us"] * kern[k]["launches"]) if kern else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if dom and os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            entry = pmc.get("kernels", {}).get(dom)
+            if entry and pmc.get("n") == n and pmc.get("alphabet") == args.alphabet:
+                traffic = entry.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = None
+    if dom:
+        ach = kern[dom]["achieved_GBps"]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "algo_bytes_per_launch": kern[dom]["algo_bytes"]}
+
+    # ---- PCIe-inclusive host path (reported, never the value) ----
+    host_path = None
+    if rank == 0 and world == 1 and not args.no_host_path:
+        from nghttp3_amd import qpack_huffman as q
+        e_host = enc[:enc_bytes].cpu().numpy()
+        sp = np.zeros(n, dtype=q.SPAN_IN_DTYPE)
+        eo = eout.cpu().numpy()
+        sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+        reps = 3
+        codec.decode_host(e_host, sp)  # warm the staging buffers
+        a = time.perf_counter()
+        for _ in range(reps):
+            codec.decode_host(e_host, sp)
+        t_host = (time.perf_counter() - a) / reps
+        host_path = {"decode_GiBps_incl_h2d_d2h": round(total / t_host / GIB, 2),
+                     "ms": round(t_host * 1e3, 2), "note": "pageable host buffers"}
+
+    # ---- CPU baseline (rank 0, N = 1) ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        plain = src[:total].cpu().numpy()
+        sp = spans.cpu().numpy()
+        off = sp[:, 0].astype(np.uint64)
+        lens = (sp[:, 1] & 0xFFFFFFFF).astype(np.uint32)
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except Exception:
+            aff = os.cpu_count() or 1
+        threads = args.cpu_threads or min(16, aff)
+        e_s, d_s, cok = oracle.bench_roundtrip(plain, off, lens, threads, args.cpu_reps)
+        cpu = {"value": round(total * args.cpu_reps / (e_s + d_s) / GIB, 4), "unit": "GiB/s",
+               "cores": threads, "kind": "port",
+               "sample": f"all {n} strings x {args.cpu_reps} round trips "
+                         f"({total * args.cpu_reps / 1e9:.2f} GB plaintext), {threads} pthreads, "
+                         f"oracle/qh_oracle.c -O2 -mavx2, ok={cok}",
+               "decode_GiBps": round(total * args.cpu_reps / d_s / GIB, 4),
+               "encode_GiBps": round(total * args.cpu_reps / e_s / GIB, 4),
+               "cpu_model": _cpu_model()}
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s device-resident QPACK Huffman encode+decode, 1M strings; bit-exact",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed_max / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64, nghttp3_amd/synth.py)",
+            "config": {"workload": "config 3: Huffman encode+decode round trip, 2^20 strings "
+                                   f"{args.lo}-{args.hi} B, alphabet {args.alphabet}, per GPU",
+                       "strings_per_gpu": n, "plain_bytes_per_gpu": total,
+                       "enc_bytes_per_gpu": enc_bytes, "seed": hex(args.seed),
+                       "parallelism": f"shard{world}"},
+            "bit_exact": bad == 0,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "extra": {"decode_GiBps": round(total / t_dec / GIB, 2),
+                      "encode_GiBps": round(total / t_enc / GIB, 2),
+                      "kernels": kern, "host_path": host_path},
+        }
+        print(json.dumps(line))
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP batch path (qh_decode_batch / qh_encode_count_batch /
+qh_encode_batch through the C ABI) against the oracle and the committed
+fixtures.  Integer/byte work, so every comparison is bit-exact."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import strings_of
+from nghttp3_amd import qpack_huffman as q
+from nghttp3_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def torch_mod():
+    import torch
+    return torch
+
+
+def to_dev(a, dtype=None):
+    torch = torch_mod()
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.view(dtype)
+    return t.cuda()
+
+
+def spans_dev(off, ln):
+    sp = np.zeros((len(ln), 2), dtype=np.int64)
+    sp[:, 0] = np.asarray(off, dtype=np.int64)
+    sp[:, 1] = np.asarray(ln, dtype=np.int64)
+    return to_dev(sp)
+
+
+def decode_dev(codec, enc, off, ln, cap=None):
+    torch = torch_mod()
+    n = len(ln)
+    slots = int((np.asarray(ln, dtype=np.int64) * 8 // 5).sum())
+    cap = slots if cap is None else cap
+    src = to_dev(enc if len(enc) else np.zeros(1, np.uint8))
+    dst = torch.zeros(max(cap, 1), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(src, spans_dev(off, ln), dst[:cap] if cap else dst[:0], out)
+    o, l, s = q.unpack_out(out)
+    return dst.cpu().numpy(), o, l, s
+
+
+def encode_dev(codec, plain, off, ln):
+    torch = torch_mod()
+    n = len(ln)
+    bound = int(((np.asarray(ln, dtype=np.int64) * 30 + 7) // 8).sum())
+    src = to_dev(plain if len(plain) else np.zeros(1, np.uint8))
+    dst = torch.zeros(max(bound, 1), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans_dev(off, ln), dst, out)
+    o, l, s = q.unpack_out(out)
+    return dst.cpu().numpy(), o, l, s
+
+
+def test_kat(codec, kat):
+    strs = [bytes.fromhex(v["huffman_hex"]) for v in kat]
+    src, sp = q.pack_strings(strs)
+    dst, o, l, s = decode_dev(codec, src, sp["off"], sp["len"])
+    for i, v in enumerate(kat):
+        assert s[i] == 0
+        assert dst[o[i]:o[i] + l[i]].tobytes() == v["plain"].encode()
+    plains = [v["plain"].encode() for v in kat]
+    src, sp = q.pack_strings(plains)
+    enc, o, l, s = encode_dev(codec, src, sp["off"], sp["len"])
+    for i, v in enumerate(kat):
+        assert enc[o[i]:o[i] + l[i]].tobytes().hex() == v["huffman_hex"]
+
+
+def test_corpus_decode(codec, corpus):
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
+    dst, o, l, s = decode_dev(codec, enc, eoff, elen)
+    assert (s == 0).all()
+    assert (o == want_slot.astype(np.int64)).all()
+    assert (l == want_len.astype(np.int64)).all()
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    for i in range(len(ln)):
+        assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes(), i
+
+
+def test_corpus_encode(codec, corpus):
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    enc, o, l, s = encode_dev(codec, plain, off, ln)
+    assert (s == 0).all()
+    assert (l == corpus["enc_len"].astype(np.int64)).all()
+    assert (o == corpus["enc_off"].astype(np.int64)).all()
+    total = int(corpus["enc_len"].astype(np.int64).sum())
+    assert (enc[:total] == corpus["enc"]).all()
+
+
+def test_corpus_encode_count(codec, corpus):
+    torch = torch_mod()
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    hlen = torch.zeros(len(ln), dtype=torch.int32, device="cuda")
+    codec.encode_count_dev(to_dev(plain), spans_dev(off, ln), hlen)
+    assert (hlen.cpu().numpy().astype(np.int64) == corpus["enc_len"].astype(np.int64)).all()
+
+
+def test_corrupted_statuses(codec, corpus):
+    bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+    dst, o, l, s = decode_dev(codec, bad, boff, blen)
+    assert (s == corpus["bad_status"].astype(np.int64)).all()
+    assert (l == corpus["bad_out_len"].astype(np.int64)).all()
+    bo = corpus["bad_out"]
+    pos = 0
+    for i in range(len(blen)):
+        n = int(corpus["bad_out_len"][i])
+        if s[i] == 0:
+            assert dst[o[i]:o[i] + n].tobytes() == bo[pos:pos + n].tobytes()
+        pos += n
+
+
+def test_error_fixture(codec, errors):
+    strs = [bytes.fromhex(c["hex"]) for c in errors["whole"]]
+    src, sp = q.pack_strings(strs)
+    dst, o, l, s = decode_dev(codec, src, sp["off"], sp["len"])
+    for i, c in enumerate(errors["whole"]):
+        assert s[i] == c["status"], c
+        if c["status"] == 0:
+            assert dst[o[i]:o[i] + l[i]].tobytes().hex() == c["out_hex"]
+
+
+def test_empty_batch_and_empty_strings(codec):
+    torch = torch_mod()
+    src = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    sp = torch.zeros((0, 2), dtype=torch.int64, device="cuda")
+    out = torch.zeros((0, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(src, sp, src, out)
+    codec.encode_dev(src, sp, src, out)
+    codec.sync()
+    dst, o, l, s = decode_dev(codec, np.zeros(4, np.uint8), [0, 1, 2], [0, 0, 0])
+    assert (s == 0).all() and (l == 0).all()
+
+
+def test_unordered_overlapping_spans(codec, corpus):
+    # spans need not be packed or monotone: reverse order, duplicates, gaps.
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    rng = np.random.default_rng(11)
+    idx = rng.permutation(len(elen))[:1500]
+    idx = np.concatenate([idx, idx[:100]])
+    dst, o, l, s = decode_dev(codec, enc, eoff[idx], elen[idx])
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    for j, i in enumerate(idx):
+        assert s[j] == 0
+        assert dst[o[j]:o[j] + l[j]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes()
+
+
+def test_dst_cap_too_small(codec, corpus):
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    n = 300
+    slots = (elen[:n].astype(np.int64) * 8 // 5)
+    cap = int(slots[:150].sum())
+    dst, o, l, s = decode_dev(codec, enc, eoff[:n], elen[:n], cap=cap)
+    fits = (o + slots) <= cap
+    assert (s[fits] == 0).all()
+    assert (s[~fits] == q.QH_ERR_NOMEM).all()
+
+
+def test_host_path_matches(codec, corpus):
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    sp = np.zeros(len(elen), dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eoff, elen
+    dst, out = codec.decode_host(enc, sp)
+    want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
+    assert (out["status"] == 0).all() and (out["len"] == want_len).all()
+    assert (out["off"] == want_slot).all()
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    psp = np.zeros(len(ln), dtype=q.SPAN_IN_DTYPE)
+    psp["off"], psp["len"] = off, ln
+    e2, eout = codec.encode_host(plain, psp)
+    total = int(corpus["enc_len"].astype(np.int64).sum())
+    assert (e2[:total] == corpus["enc"]).all()
+    st = codec.stats()
+    assert st["n"] == len(ln) and st["out_bytes"] == total
+    assert (codec.encode_count_host(plain, psp) == corpus["enc_len"]).all()
+
+
+def test_synth_device_matches_host(codec):
+    src, spans, total = codec.synth(0x1234, 5000, 1, 300, synth.ALPHABET_A)
+    plain, off, ln = synth.batch(0x1234, 5000, 1, 300, synth.ALPHABET_A)
+    sp = spans.cpu().numpy()
+    assert total == plain.size
+    assert (sp[:, 0] == off.astype(np.int64)).all()
+    assert ((sp[:, 1] & 0xFFFFFFFF) == ln.astype(np.int64)).all()
+    assert (src.cpu().numpy()[:total] == plain).all()
+
+
+@pytest.mark.parametrize("name", ["c2_A", "c2_U", "c3_A"])
+def test_full_size_config(codec, digests, name):
+    """BASELINE configs at full size (2^20 strings): synth digest, encode
+    digest vs the oracle's, then decode round trip (size-independent)."""
+    torch = torch_mod()
+    d = digests[name]
+    alph = synth.ALPHABET_A if d["alphabet"] == "A" else synth.ALPHABET_U
+    src, spans, total = codec.synth(d["seed"], d["n"], d["lo"], d["hi"], alph)
+    assert total == d["plain_bytes"]
+    assert sha(src[:total].cpu().numpy()) == d["plain_sha256"]
+    n = d["n"]
+    ln = spans[:, 1] & 0xFFFFFFFF
+    bound = int(((ln * 30 + 7) // 8).sum().item())
+    enc = torch.zeros(bound, dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    st = codec.stats()
+    assert st["n_errors"] == 0 and st["out_bytes"] == d["enc_bytes"]
+    elen = (eout[:, 1] & 0xFFFFFFFF).to(torch.int32)
+    assert sha(elen.cpu().numpy().astype(np.uint32)) == d["enc_len_sha256"]
+    assert sha(enc[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
+    # decode what we encoded: encode's out spans are valid decode in spans
+    cap = int(((elen.to(torch.int64) * 8) // 5).sum().item())
+    dec = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    dout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(enc, eout, dec, dout)
+    st = codec.stats()
+    assert st["n_errors"] == 0 and st["out_bytes"] == total
+    dlen = dout[:, 1] & 0xFFFFFFFF
+    assert bool((dlen == ln).all())
+    assert bool(((dout[:, 1] >> 32) == 0).all())
+    # gather decoded bytes in string order and compare with the plaintext
+    doff = dout[:, 0]
+    poff = spans[:, 0]
+    rep_d = torch.repeat_interleave(doff, ln)
+    rep_p = torch.repeat_interleave(poff, ln)
+    pos = torch.arange(total, device="cuda", dtype=torch.int64) - rep_p
+    assert bool((dec[rep_d + pos] == src[:total]).all())
