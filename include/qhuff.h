@@ -148,8 +148,9 @@ typedef struct qh_batch_stats {
 
 typedef struct qh_ctx qh_ctx;
 
-/* Bind a context to HIP device `device` and stream `stream` (a hipStream_t,
- * or NULL to let the library create a non-blocking stream). */
+/* Bind a context to HIP device `device` and stream `stream` (a hipStream_t;
+ * NULL = the device's default stream, as in other HIP libraries).  Every
+ * batch call is ordered on that stream. */
 QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream);
 QH_EXPORT void qh_ctx_del(qh_ctx *ctx);
 QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);

@@ -835,14 +835,8 @@ QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess &&
       prop.multiProcessorCount > 0)
     c->num_cus = prop.multiProcessorCount;
-  if (stream) {
-    c->stream = (hipStream_t)stream;
-  } else {
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) !=
-        hipSuccess)
-      return fail(QH_ERR_FATAL);
-    c->own_stream = true;
-  }
+  // NULL selects the HIP default (null) stream, as HIP/ROCm libraries do.
+  c->stream = (hipStream_t)stream;
   if (hipMalloc(&c->d_fsm, sizeof(kFsmPacked)) != hipSuccess ||
       hipMalloc(&c->d_sym, sizeof(kSymPacked)) != hipSuccess ||
       hipMalloc(&c->d_stats, sizeof(DevStats)) != hipSuccess)
@@ -860,7 +854,7 @@ QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream) {
 QH_EXPORT void qh_ctx_del(qh_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  hipStreamSynchronize(c->stream);
   for (auto &e : c->events) {
     hipEventDestroy(e.a);
     hipEventDestroy(e.b);
@@ -879,16 +873,11 @@ QH_EXPORT void qh_ctx_del(qh_ctx *c) {
 QH_EXPORT int qh_ctx_set_stream(qh_ctx *c, void *stream) {
   if (!c) return QH_ERR_INVALID_ARGUMENT;
   if (c->own_stream && c->stream) {
-    hipStreamSynchronize(c->stream);
-    hipStreamDestroy(c->stream);
-    c->own_stream = false;
+    QH_HIP(hipStreamSynchronize(c->stream));
+    QH_HIP(hipStreamDestroy(c->stream));
   }
-  if (stream) {
-    c->stream = (hipStream_t)stream;
-  } else {
-    QH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    c->own_stream = true;
-  }
+  c->own_stream = false;
+  c->stream = (hipStream_t)stream;
   return 0;
 }
 

@@ -127,21 +127,20 @@ def _torch():
 class HuffmanBatchCodec:
     """A qh_ctx bound to one HIP device and stream.
 
-    ``stream``: a torch.cuda.Stream, a raw hipStream_t integer, or None for
-    torch's current stream on ``device`` (so torch events time the kernels).
+    ``stream``: a torch.cuda.Stream, a raw hipStream_t integer (0 = the
+    default stream), or None for torch's current stream on ``device`` (so
+    torch's synchronisation and events cover the kernels).
     """
 
-    def __init__(self, device: int = 0, stream=None, own_stream: bool = False):
+    def __init__(self, device: int = 0, stream=None):
         self._lib = _lib.load()
-        handle = None
-        if not own_stream:
-            if stream is None:
-                torch = _torch()
-                handle = torch.cuda.current_stream(device).cuda_stream
-            elif isinstance(stream, int):
-                handle = stream
-            else:
-                handle = stream.cuda_stream
+        if stream is None:
+            torch = _torch()
+            handle = torch.cuda.current_stream(device).cuda_stream
+        elif isinstance(stream, int):
+            handle = stream
+        else:
+            handle = stream.cuda_stream
         ctx = ctypes.c_void_p()
         _lib.check(self._lib.qh_ctx_new(ctypes.byref(ctx), device,
                                         ctypes.c_void_p(handle) if handle else None),

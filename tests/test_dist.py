@@ -1,0 +1,79 @@
+"""World-size-2 gloo run of the sharded path (CPU): each rank takes its
+byte-balanced contiguous shard of one batch, encodes/decodes it alone (the
+oracle stands in for the device here), and only the report crosses ranks.
+The reduced report must equal the single-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from nghttp3_amd import shard, synth
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        plain, off, ln = synth.batch(synth.SEEDS[4], 20000, 1, 400, synth.ALPHABET_A)
+        b, e = shard.split_by_bytes(ln, world)[rank]
+        enc, eoff, elen = oracle.encode_batch(plain, off[b:e], ln[b:e])
+        dst, slot, olen, st = oracle.decode_batch(enc, eoff, elen)
+        local = {"strings": e - b, "plain_bytes": int(ln[b:e].sum()), "enc_bytes": int(enc.size),
+                 "errors": int((st != 0).sum()) + int((olen != ln[b:e]).sum()),
+                 "time_max": float(rank + 1)}
+        rep = shard.reduce_report(local, dist)
+        base = shard.output_offsets(int(enc.size), dist)
+        q.put((rank, b, e, base, rep, enc.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_roundtrip_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle
+    plain, off, ln = synth.batch(synth.SEEDS[4], 20000, 1, 400, synth.ALPHABET_A)
+    enc, eoff, elen = oracle.encode_batch(plain, off, ln)
+    # shards tile the batch, in order, with near-equal bytes
+    assert res[0][1] == 0 and res[-1][2] == len(ln)
+    assert all(res[i][2] == res[i + 1][1] for i in range(world - 1))
+    sizes = [int(ln[b:e].sum()) for _, b, e, *_ in res]
+    assert max(sizes) - min(sizes) <= 2 * 400  # one string either side of a cut
+    # global output offsets come from the all-gather; shards concatenate
+    assert [r[3] for r in res] == [0] + list(np.cumsum([len(r[5]) for r in res])[:-1])
+    assert b"".join(r[5] for r in res) == enc.tobytes()
+    rep = res[0][4]
+    assert rep == res[1][4]
+    assert rep["strings"] == len(ln) and rep["plain_bytes"] == int(ln.sum())
+    assert rep["enc_bytes"] == enc.size and rep["errors"] == 0 and rep["time_max"] == world
+
+
+def test_split_by_bytes_edges():
+    assert shard.split_by_bytes([], 4) == [(0, 0)] * 4
+    assert shard.split_by_bytes([5], 3) == [(0, 0), (0, 0), (0, 1)] or \
+        sum(e - b for b, e in shard.split_by_bytes([5], 3)) == 1
+    r = shard.split_by_bytes([1] * 10, 3)
+    assert r[0][0] == 0 and r[-1][1] == 10
+    assert sum(e - b for b, e in r) == 10
