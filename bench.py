@@ -65,6 +65,7 @@ def main():
     import torch.distributed as dist
 
     from nghttp3_amd import HuffmanBatchCodec, synth
+    from nghttp3_amd import qpack_huffman as q
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -97,7 +98,7 @@ def main():
     torch.cuda.synchronize()
     elen = eout[:, 1] & 0xFFFFFFFF
     enc_bytes = int(elen.sum().item())
-    dec_cap = int(((elen * 8) // 5).sum().item())
+    dec_cap = int(q.decode_slot_size(elen).sum().item())
     dec = torch.empty(max(dec_cap, 1), dtype=torch.uint8, device=dev)
 
     def step():
@@ -190,7 +191,6 @@ def main():
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None
     if rank == 0 and world == 1 and not args.no_host_path:
-        from nghttp3_amd import qpack_huffman as q
         e_host = enc[:enc_bytes].cpu().numpy()
         sp = np.zeros(n, dtype=q.SPAN_IN_DTYPE)
         eo = eout.cpu().numpy()

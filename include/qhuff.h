@@ -160,12 +160,14 @@ QH_EXPORT int qh_ctx_sync(qh_ctx *ctx);
 /* Totals of the last batch call (synchronises the stream). */
 QH_EXPORT int qh_ctx_last_stats(qh_ctx *ctx, qh_batch_stats *stats);
 
-/* Destination sizing.  Decode uses the reference's ownership convention:
- * string i owns a slot of nghttp3_qpack_huffman_estimate_decode_length(len)
- * bytes (the rcbuf the reference allocates at qpack.c:2977,3065,3591,3677,
- * minus the NUL), slots laid out back to back in string order, so
- * out[i].off = sum_{j<i} in[j].len * 8 / 5 and dst_cap must be at least
- * qh_decode_dst_size(in, n).  Encode output is dense: out[i].off = sum_{j<i}
+/* Destination sizing.  Decode follows the reference's ownership convention:
+ * string i owns a slot sized by nghttp3_qpack_huffman_estimate_decode_length
+ * (the rcbuf the reference allocates at qpack.c:2977,3065,3591,3677, minus
+ * the NUL), rounded up to 16 bytes so every slot starts 16-byte aligned:
+ *   slot(len) = round_up(len * 8 / 5, 16),
+ * slots back to back in string order, out[i].off = sum_{j<i} slot(in[j].len),
+ * dst_cap >= qh_decode_dst_size(in, n).  Bytes of a slot past out[i].len are
+ * unspecified.  Encode output is dense: out[i].off = sum_{j<i}
  * encode_count(string j); qh_encode_dst_bound() is an upper bound. */
 QH_EXPORT uint64_t qh_decode_dst_size(const qh_span_in *in, size_t n);
 QH_EXPORT uint64_t qh_encode_dst_bound(const qh_span_in *in, size_t n);

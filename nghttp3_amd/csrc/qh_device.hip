@@ -127,10 +127,12 @@ struct Sink {
   uint32_t head;     // leading bytes of *wp that belong to someone else
 };
 
+// Pointer arithmetic (not integer casts) keeps the global address space, so
+// stores stay global_store_* rather than flat_* (flat ops also count on
+// lgkmcnt and would make every LDS lookup of the FSM wait for them).
 __device__ __forceinline__ void sink_init(Sink &s, uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  s.wp = reinterpret_cast<uint32_t *>(a & ~uintptr_t(3));
-  s.head = (uint32_t)(a & 3);
+  s.head = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  s.wp = reinterpret_cast<uint32_t *>(p - s.head);
   s.acc = 0;
   s.nb = s.head * 8;
 }
@@ -194,6 +196,12 @@ __device__ __forceinline__ u32x4 load_tail(const uint8_t *p, uint32_t pos,
 // decoupled look-back exclusive scan over strings
 // ---------------------------------------------------------------------------
 
+// Decode slot of a string with `len` encoded bytes: the reference's
+// estimate_decode_length (huffman.h:113-115) rounded up to 16 bytes.
+__host__ __device__ __forceinline__ uint64_t qh_slot_size(uint32_t len) {
+  return (((uint64_t)len * 8 / 5) + 15) & ~uint64_t(15);
+}
+
 constexpr int kScanItems = 8;
 constexpr int kScanTile = kBlock * kScanItems;  // 2048 strings per tile
 constexpr uint64_t kStA = 1ull << 62;           // aggregate available
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void qh_k_scan(
     uint64_t v = 0;
     if (i < n) {
       if (MODE == SCAN_SLOTS)
-        v = (uint64_t)in[i].len * 8 / 5;
+        v = qh_slot_size(in[i].len);
       else
         v = out[i].len;
     }
@@ -333,21 +341,31 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
     const uint64_t slot = out[s].off;
     const uint32_t len = sp.len;
     my_in += len;
-    if (slot + (uint64_t)len * 8 / 5 > dst_cap) {
+    if (slot + qh_slot_size(len) > dst_cap) {
       out[s].len = 0;
       out[s].status = QH_ERR_NOMEM;
       ++my_err;
       continue;
     }
     const uint8_t *p = src + sp.off;
-    uint8_t *q = dst + slot;
-    Sink sink;
-    sink_init(sink, q);
-    uint64_t acc = sink.acc;
-    uint32_t nb = sink.nb;
+    // Slots are 16-byte aligned (qh_slot_size), so the string's output is
+    // written with whole aligned dwords only: no head bytes, and the last
+    // partial dword spills garbage into the string's own slot padding.
+    uint32_t *wp = reinterpret_cast<uint32_t *>(dst + slot);
+    uint64_t acc = 0;
+    uint32_t nb = 0;
+    uint32_t nout = 0;                       // dwords stored
     uint32_t st = 0;
     uint32_t last = QH_FLAG_ACCEPTED << 16;  // huffman.c:80-85
-    uint32_t wrote = 0;                      // dwords flushed
+
+#define QH_FLUSH()                                                            \
+  do {                                                                        \
+    if (nb >= 32) {                                                           \
+      wp[nout++] = (uint32_t)acc;                                             \
+      acc >>= 32;                                                             \
+      nb -= 32;                                                               \
+    }                                                                         \
+  } while (0)
 
     uint32_t pos = 0;
     const uint32_t body = len & ~15u;
@@ -358,14 +376,10 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
         const uint32_t w = v[d];
         QH_DECODE_BYTE(w, 0);
         QH_DECODE_BYTE(w, 1);
-        sink.acc = acc; sink.nb = nb;
-        if (nb >= 32) { sink_flush(sink); ++wrote; }
-        acc = sink.acc; nb = sink.nb;
+        QH_FLUSH();
         QH_DECODE_BYTE(w, 2);
         QH_DECODE_BYTE(w, 3);
-        sink.acc = acc; sink.nb = nb;
-        if (nb >= 32) { sink_flush(sink); ++wrote; }
-        acc = sink.acc; nb = sink.nb;
+        QH_FLUSH();
       }
     }
     if (pos < len) {
@@ -378,22 +392,18 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
         for (int b = 0; b < 4; ++b) {
           if ((uint32_t)(4 * d + b) < rem) {
             QH_DECODE_BYTE(w, b);
-            sink.acc = acc; sink.nb = nb;
-            if (nb >= 32) { sink_flush(sink); ++wrote; }
-            acc = sink.acc; nb = sink.nb;
+            QH_FLUSH();
           }
         }
       }
     }
-    sink.acc = acc;
-    sink.nb = nb;
-    const uint32_t head0 = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 3);
-    const uint32_t dec_len = wrote * 4 + (nb >> 3) - head0;
+#undef QH_FLUSH
+    const uint32_t dec_len = nout * 4 + (nb >> 3);
     // huffman.c:119-121: fin && !ACCEPTED -> -108.  The absorbing failure
     // state 256 carries no flags, so it fails here too (qpack.c:2756).
     const bool ok = (last >> 16) & QH_FLAG_ACCEPTED;
     if (ok) {
-      sink_finish(sink);
+      if (nb) wp[nout] = (uint32_t)acc;
       out[s].len = dec_len;
       out[s].status = 0;
       my_out += dec_len;
@@ -458,6 +468,11 @@ __global__ __launch_bounds__(kBlock) void qh_k_count(
   block_add(&stats->in_bytes, my_in, red);
 }
 
+// The bit accumulator is pre-loaded with `head` dummy bytes (the bytes of
+// the first aligned dword that belong to the previous string), so every
+// 32-bit word it emits is an aligned dword of dst.  The first word is shared
+// with the previous string and is kept in a register; all later words are
+// stored whole.  Only the two edge dwords are written bytewise, once.
 #define QH_ENCODE_SYM(c)                                                      \
   do {                                                                        \
     const uint2 e = symtab[(c)];                                              \
@@ -465,9 +480,9 @@ __global__ __launch_bounds__(kBlock) void qh_k_count(
     nbits += e.x;                                                             \
     if (nbits >= 32) {                                                        \
       const uint32_t x = (uint32_t)(code >> 32);                              \
-      sink.acc |= (uint64_t)__builtin_bswap32(x) << sink.nb;                  \
-      sink.nb += 32;                                                          \
-      sink_flush(sink);                                                       \
+      if (k == 0) first = x;                                                  \
+      if (k != 0 || head == 0) wp[k] = __builtin_bswap32(x);                  \
+      ++k;                                                                    \
       code <<= 32;                                                            \
       nbits -= 32;                                                            \
     }                                                                         \
@@ -496,10 +511,12 @@ __global__ __launch_bounds__(kBlock) void qh_k_encode(
     }
     const uint8_t *p = src + sp.off;
     const uint32_t len = sp.len;
-    Sink sink;
-    sink_init(sink, dst + so.off);
+    const uint32_t head = (uint32_t)(so.off & 3);
+    uint32_t *wp = reinterpret_cast<uint32_t *>(dst + so.off - head);
     uint64_t code = 0;
-    uint32_t nbits = 0;
+    uint32_t nbits = head * 8;  // dummy leading bits, never stored
+    uint32_t k = 0;             // aligned dwords emitted
+    uint32_t first = 0;         // big-endian image of dword 0
     uint32_t pos = 0;
     const uint32_t body = len & ~15u;
     for (; pos < body; pos += 16) {
@@ -519,21 +536,24 @@ __global__ __launch_bounds__(kBlock) void qh_k_encode(
           if ((uint32_t)(4 * d + b) < rem)
             QH_ENCODE_SYM((v[d] >> (8 * b)) & 0xFFu);
     }
-    // huffman.c:67-75: whole bytes, then the last partial byte padded with
-    // the most significant bits of EOS (all ones).
-    for (; nbits >= 8; nbits -= 8) {
-      sink.acc |= (uint64_t)(uint8_t)(code >> 56) << sink.nb;
-      sink.nb += 8;
-      code <<= 8;
+    // huffman.c:67-75: pad the last partial byte with the leading (all-one)
+    // bits of EOS; nbits < 32 here.
+    const uint32_t padded = (nbits + 7) & ~7u;
+    if (padded != nbits)
+      code |= ((1ull << (padded - nbits)) - 1) << (64 - padded);
+    const uint32_t tail = (uint32_t)(code >> 32);  // bytes [0, padded/8)
+    uint8_t *b0 = reinterpret_cast<uint8_t *>(wp);
+    if (k == 0) {
+      // the whole string lies inside dword 0: bytes [head, padded/8)
+      for (uint32_t j = head; j < padded / 8; ++j)
+        b0[j] = (uint8_t)(tail >> (24 - 8 * j));
+    } else {
+      for (uint32_t j = head; j < 4 && head; ++j)
+        b0[j] = (uint8_t)(first >> (24 - 8 * j));
+      uint8_t *bk = b0 + 4 * k;
+      for (uint32_t j = 0; j < padded / 8; ++j)
+        bk[j] = (uint8_t)(tail >> (24 - 8 * j));
     }
-    if (nbits) {
-      const uint8_t last =
-          (uint8_t)((uint8_t)(code >> 56) | ((1u << (8 - nbits)) - 1));
-      sink.acc |= (uint64_t)last << sink.nb;
-      sink.nb += 8;
-    }
-    if (sink.nb >= 32) sink_flush(sink);
-    sink_finish(sink);
     my_out += so.len;
   }
   block_add(&stats->out_bytes, my_out, red);
@@ -913,7 +933,7 @@ QH_EXPORT int qh_ctx_last_stats(qh_ctx *c, qh_batch_stats *st) {
 
 QH_EXPORT uint64_t qh_decode_dst_size(const qh_span_in *in, size_t n) {
   uint64_t s = 0;
-  for (size_t i = 0; i < n; ++i) s += (uint64_t)in[i].len * 8 / 5;
+  for (size_t i = 0; i < n; ++i) s += qh_slot_size(in[i].len);
   return s;
 }
 

@@ -56,6 +56,13 @@ def huffman_estimate_decode_length(n: int) -> int:
     return n * 8 // 5
 
 
+def decode_slot_size(n):
+    """Bytes a string of n encoded bytes owns in the batch decode output:
+    estimate_decode_length rounded up to 16 (include/qhuff.h).  Works on ints
+    and on numpy / torch integer arrays."""
+    return ((n * 8 // 5) + 15) // 16 * 16
+
+
 def huffman_encode_count(src) -> int:
     """lib/nghttp3_qpack_huffman.c:34-43"""
     p, n, _keep = _buf(src)
@@ -275,7 +282,7 @@ def unpack_out(out):
 
 __all__ = [
     "NGHTTP3_ERR_QPACK_FATAL", "QH_ERR_NOMEM", "QhError", "HuffmanDecodeContext",
-    "huffman_estimate_decode_length", "huffman_encode_count", "huffman_encode",
+    "huffman_estimate_decode_length", "decode_slot_size", "huffman_encode_count", "huffman_encode",
     "huffman_decode_context_init", "huffman_decode", "huffman_decode_failure_state",
     "HuffmanBatchCodec", "pack_strings", "unpack_out", "SPAN_IN_DTYPE", "SPAN_OUT_DTYPE",
 ]

@@ -135,7 +135,7 @@ def decode_batch(enc, off, ln):
     off = np.ascontiguousarray(off, dtype=np.uint64)
     ln = np.ascontiguousarray(ln, dtype=np.uint32)
     n = ln.size
-    cap = int((ln.astype(np.uint64) * 8 // 5).sum()) + 16
+    cap = int((((ln.astype(np.uint64) * 8 // 5) + 15) // 16 * 16).sum()) + 16
     dst = np.zeros(cap, dtype=np.uint8)
     slot = np.zeros(max(n, 1), dtype=np.uint64)
     olen = np.zeros(max(n, 1), dtype=np.uint32)

@@ -267,7 +267,7 @@ uint64_t qho_decode_batch(const uint8_t *src, const uint64_t *off,
       out_len[i] = (uint32_t)r;
       status[i] = 0;
     }
-    slot += (uint64_t)len[i] * 8 / 5;
+    slot += ((uint64_t)len[i] * 8 / 5 + 15) & ~(uint64_t)15; /* qhuff.h slot */
   }
   return nerr;
 }

@@ -57,7 +57,8 @@ int qho_decode_failure_state(const qho_decode_ctx *ctx);
  * encode: writes encoded strings densely into dst; out_off/out_len per string
  *   (out_off = exclusive prefix sum of encode_count). Returns total bytes.
  * decode (fin = 1 per string): string i written at dst + slot_off[i] where
- *   slot_off is the exclusive prefix sum of len*8/5 (huffman.h:113-115);
+ *   slot_off is the exclusive prefix sum of the batch API's slot size,
+ *   round_up(len*8/5, 16) (huffman.h:113-115 estimate, include/qhuff.h);
  *   out_len = decoded length (0 on error), status 0 or -108. Returns the
  *   number of failed strings. */
 uint64_t qho_encode_batch(const uint8_t *src, const uint64_t *off,

@@ -9,7 +9,7 @@ encs = [oracle.encode(s) for s in strs]
 src, sp = pack_strings(encs)
 d_src = torch.from_numpy(src.copy()).cuda()
 d_sp = torch.from_numpy(sp.view(np.int64).reshape(-1, 2).copy()).cuda()
-cap = int((sp["len"].astype(np.int64) * 8 // 5).sum())
+cap = int((((sp["len"].astype(np.int64) * 8 // 5) + 15) // 16 * 16).sum())
 d_dst = torch.zeros(cap + 64, dtype=torch.uint8, device="cuda")
 d_out = torch.zeros((len(strs), 2), dtype=torch.int64, device="cuda")
 codec.decode_dev(d_src, d_sp, d_dst[:cap], d_out)

@@ -41,7 +41,7 @@ def spans_dev(off, ln):
 def decode_dev(codec, enc, off, ln, cap=None):
     torch = torch_mod()
     n = len(ln)
-    slots = int((np.asarray(ln, dtype=np.int64) * 8 // 5).sum())
+    slots = int(q.decode_slot_size(np.asarray(ln, dtype=np.int64)).sum())
     cap = slots if cap is None else cap
     src = to_dev(enc if len(enc) else np.zeros(1, np.uint8))
     dst = torch.zeros(max(cap, 1), dtype=torch.uint8, device="cuda")
@@ -159,7 +159,7 @@ def test_unordered_overlapping_spans(codec, corpus):
 def test_dst_cap_too_small(codec, corpus):
     enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
     n = 300
-    slots = (elen[:n].astype(np.int64) * 8 // 5)
+    slots = q.decode_slot_size(elen[:n].astype(np.int64))
     cap = int(slots[:150].sum())
     dst, o, l, s = decode_dev(codec, enc, eoff[:n], elen[:n], cap=cap)
     fits = (o + slots) <= cap
@@ -218,7 +218,7 @@ def test_full_size_config(codec, digests, name):
     assert sha(elen.cpu().numpy().astype(np.uint32)) == d["enc_len_sha256"]
     assert sha(enc[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
     # decode what we encoded: encode's out spans are valid decode in spans
-    cap = int(((elen.to(torch.int64) * 8) // 5).sum().item())
+    cap = int(q.decode_slot_size(elen.to(torch.int64)).sum().item())
     dec = torch.zeros(cap, dtype=torch.uint8, device="cuda")
     dout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
     codec.decode_dev(enc, eout, dec, dout)
