@@ -298,13 +298,61 @@ __global__ __launch_bounds__(kBlock) void qh_k_scan(
 }
 
 // ---------------------------------------------------------------------------
+// tile scheduling: one block = 256 strings, one lane each, ranked by length
+// ---------------------------------------------------------------------------
+
+struct TileLds {
+  uint32_t hist[kBlock];
+  uint32_t order[kBlock];
+  uint32_t wsum[kBlock / 64];
+};
+
+// Counting-sort the tile's strings by length (longest first, 16-byte
+// buckets) so that the 64 lanes of a wave get similar trip counts; returns
+// the tile-relative index of the string this thread processes.  The
+// permutation only changes which lane decodes a string, never its output.
+__device__ __forceinline__ uint32_t tile_rank_by_len(uint32_t len, TileLds &t) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t key = 255u - min(len >> 4, 255u);
+  t.hist[tid] = 0;
+  __syncthreads();
+  const uint32_t r = atomicAdd(&t.hist[key], 1u);
+  __syncthreads();
+  const uint32_t h = t.hist[tid];
+  uint32_t incl = h;
+  const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o);
+    if (lane >= o) incl += x;
+  }
+  if (lane == 63) t.wsum[wid] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w)
+    if (w < wid) base += t.wsum[w];
+  t.hist[tid] = base + incl - h;  // bucket start
+  __syncthreads();
+  t.order[t.hist[key] + r] = tid;
+  __syncthreads();
+  return t.order[tid];
+}
+
+// ---------------------------------------------------------------------------
 // decode: one lane per string, FSM in LDS
 // ---------------------------------------------------------------------------
 
-// One FSM step for the byte `c` (= bits [8b, 8b+8) of word w).
-// LDS row layout: word = (state * 64) | flags << 16 | sym << 24, i.e. the
-// reference node {fstate, flags, sym} with fstate pre-multiplied into the
-// byte offset of its 16-entry row.
+// LDS image of the decode FSM.  Rows are padded to 17 dwords so that entry
+// (row r, nibble v) lies in bank (17 r + v) mod 32: with 16-dword rows every
+// lane reading nibble v would hit one of two banks, and header text has a
+// few dominant high nibbles (0x4-0x7).
+constexpr uint32_t kFsmRowWords = 17;
+constexpr uint32_t kFsmLdsWords = QH_NSTATE * kFsmRowWords;  // 17,476 B
+
+// One FSM step for the byte in bits [8b, 8b+8) of word w (huffman.c:103-114).
+// LDS word = (state * 68) | flags << 16 | sym << 24: the reference node
+// {fstate, flags, sym} with fstate pre-multiplied into its row's byte offset.
 #define QH_DECODE_BYTE(w, b)                                                  \
   do {                                                                        \
     const uint32_t hi4 = ((w) >> (8 * (b) + 2)) & 0x3Cu;                      \
@@ -320,23 +368,37 @@ __global__ __launch_bounds__(kBlock) void qh_k_scan(
     last = e2;                                                                \
   } while (0)
 
+#define QH_FLUSH()                                                            \
+  do {                                                                        \
+    if (nb >= 32) {                                                           \
+      wp[nout++] = (uint32_t)acc;                                             \
+      acc >>= 32;                                                             \
+      nb -= 32;                                                               \
+    }                                                                         \
+  } while (0)
+
 __global__ __launch_bounds__(kBlock) void qh_k_decode(
     const uint8_t *__restrict__ src, const SpanIn *__restrict__ in,
     SpanOut *__restrict__ out, uint64_t n, uint8_t *__restrict__ dst,
     uint64_t dst_cap, const uint32_t *__restrict__ g_fsm,
     DevStats *__restrict__ stats) {
-  __shared__ uint32_t fsm[kFsmWords];
+  __shared__ uint32_t fsm[kFsmLdsWords];
+  __shared__ TileLds tl;
   __shared__ unsigned long long red[kBlock / 64];
   for (uint32_t i = threadIdx.x; i < kFsmWords; i += kBlock) {
     const uint32_t w = g_fsm[i];
-    fsm[i] = ((w & 0xFFFFu) << 6) | (w & 0xFFFF0000u);
+    fsm[(i >> 4) * kFsmRowWords + (i & 15)] =
+        ((w & 0xFFFFu) * (kFsmRowWords * 4)) | (w & 0xFFFF0000u);
   }
   __syncthreads();
 
   unsigned long long my_in = 0, my_out = 0, my_err = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n;
-       s += stride) {
+  for (uint64_t tile0 = (uint64_t)blockIdx.x * kBlock; tile0 < n;
+       tile0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t mine = tile0 + threadIdx.x;
+    const uint32_t mylen = mine < n ? in[mine].len : 0u;
+    const uint64_t s = tile0 + tile_rank_by_len(mylen, tl);
+    if (s >= n) continue;
     const SpanIn sp = in[s];
     const uint64_t slot = out[s].off;
     const uint32_t len = sp.len;
@@ -358,19 +420,13 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
     uint32_t st = 0;
     uint32_t last = QH_FLAG_ACCEPTED << 16;  // huffman.c:80-85
 
-#define QH_FLUSH()                                                            \
-  do {                                                                        \
-    if (nb >= 32) {                                                           \
-      wp[nout++] = (uint32_t)acc;                                             \
-      acc >>= 32;                                                             \
-      nb -= 32;                                                               \
-    }                                                                         \
-  } while (0)
-
-    uint32_t pos = 0;
     const uint32_t body = len & ~15u;
-    for (; pos < body; pos += 16) {
-      const u32x4 v = *reinterpret_cast<const u32x4_ua *>(p + pos);
+    u32x4 nxt = {0, 0, 0, 0};
+    if (body) nxt = *reinterpret_cast<const u32x4_ua *>(p);
+    for (uint32_t pos = 0; pos < body; pos += 16) {
+      const u32x4 v = nxt;
+      if (pos + 16 < body)  // prefetch the next chunk before the FSM chain
+        nxt = *reinterpret_cast<const u32x4_ua *>(p + pos + 16);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t w = v[d];
@@ -382,9 +438,9 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
         QH_FLUSH();
       }
     }
-    if (pos < len) {
-      const u32x4 v = load_tail(p, pos, len);
-      const uint32_t rem = len - pos;
+    if (body < len) {
+      const u32x4 v = load_tail(p, body, len);
+      const uint32_t rem = len - body;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t w = v[d];
@@ -397,7 +453,6 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
         }
       }
     }
-#undef QH_FLUSH
     const uint32_t dec_len = nout * 4 + (nb >> 3);
     // huffman.c:119-121: fin && !ACCEPTED -> -108.  The absorbing failure
     // state 256 carries no flags, so it fails here too (qpack.c:2756).
@@ -417,6 +472,7 @@ __global__ __launch_bounds__(kBlock) void qh_k_decode(
   block_add(&stats->out_bytes, my_out, red);
   block_add(&stats->n_errors, my_err, red);
 }
+#undef QH_FLUSH
 
 // ---------------------------------------------------------------------------
 // encode_count and encode: one lane per string, symbol table in LDS
@@ -427,30 +483,36 @@ __global__ __launch_bounds__(kBlock) void qh_k_count(
     SpanOut *__restrict__ out, uint32_t *__restrict__ hlen_out, uint64_t n,
     const uint32_t *__restrict__ g_sym, DevStats *__restrict__ stats) {
   __shared__ uint8_t nbits[256];
+  __shared__ TileLds tl;
   __shared__ unsigned long long red[kBlock / 64];
   nbits[threadIdx.x] = (uint8_t)g_sym[2 * threadIdx.x];
   __syncthreads();
   unsigned long long my_in = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n;
-       s += stride) {
+  for (uint64_t tile0 = (uint64_t)blockIdx.x * kBlock; tile0 < n;
+       tile0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t mine = tile0 + threadIdx.x;
+    const uint32_t mylen = mine < n ? in[mine].len : 0u;
+    const uint64_t s = tile0 + tile_rank_by_len(mylen, tl);
+    if (s >= n) continue;
     const SpanIn sp = in[s];
     const uint8_t *p = src + sp.off;
     const uint32_t len = sp.len;
     my_in += len;
     uint32_t bits = 0;
-    uint32_t pos = 0;
     const uint32_t body = len & ~15u;
-    for (; pos < body; pos += 16) {
-      const u32x4 v = *reinterpret_cast<const u32x4_ua *>(p + pos);
+    u32x4 nxt = {0, 0, 0, 0};
+    if (body) nxt = *reinterpret_cast<const u32x4_ua *>(p);
+    for (uint32_t pos = 0; pos < body; pos += 16) {
+      const u32x4 v = nxt;
+      if (pos + 16 < body) nxt = *reinterpret_cast<const u32x4_ua *>(p + pos + 16);
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int b = 0; b < 4; ++b) bits += nbits[(v[d] >> (8 * b)) & 0xFFu];
     }
-    if (pos < len) {
-      const u32x4 v = load_tail(p, pos, len);
-      const uint32_t rem = len - pos;
+    if (body < len) {
+      const u32x4 v = load_tail(p, body, len);
+      const uint32_t rem = len - body;
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -494,13 +556,17 @@ __global__ __launch_bounds__(kBlock) void qh_k_encode(
     uint64_t dst_cap, const uint32_t *__restrict__ g_sym,
     DevStats *__restrict__ stats) {
   __shared__ uint2 symtab[256];
+  __shared__ TileLds tl;
   __shared__ unsigned long long red[kBlock / 64];
   symtab[threadIdx.x] = make_uint2(g_sym[2 * threadIdx.x], g_sym[2 * threadIdx.x + 1]);
   __syncthreads();
   unsigned long long my_out = 0, my_err = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n;
-       s += stride) {
+  for (uint64_t tile0 = (uint64_t)blockIdx.x * kBlock; tile0 < n;
+       tile0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t mine = tile0 + threadIdx.x;
+    const uint32_t mylen = mine < n ? in[mine].len : 0u;
+    const uint64_t s = tile0 + tile_rank_by_len(mylen, tl);
+    if (s >= n) continue;
     const SpanIn sp = in[s];
     const SpanOut so = out[s];
     if (so.off + so.len > dst_cap) {
@@ -517,18 +583,20 @@ __global__ __launch_bounds__(kBlock) void qh_k_encode(
     uint32_t nbits = head * 8;  // dummy leading bits, never stored
     uint32_t k = 0;             // aligned dwords emitted
     uint32_t first = 0;         // big-endian image of dword 0
-    uint32_t pos = 0;
     const uint32_t body = len & ~15u;
-    for (; pos < body; pos += 16) {
-      const u32x4 v = *reinterpret_cast<const u32x4_ua *>(p + pos);
+    u32x4 nxt = {0, 0, 0, 0};
+    if (body) nxt = *reinterpret_cast<const u32x4_ua *>(p);
+    for (uint32_t pos = 0; pos < body; pos += 16) {
+      const u32x4 v = nxt;
+      if (pos + 16 < body) nxt = *reinterpret_cast<const u32x4_ua *>(p + pos + 16);
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int b = 0; b < 4; ++b) QH_ENCODE_SYM((v[d] >> (8 * b)) & 0xFFu);
     }
-    if (pos < len) {
-      const u32x4 v = load_tail(p, pos, len);
-      const uint32_t rem = len - pos;
+    if (body < len) {
+      const u32x4 v = load_tail(p, body, len);
+      const uint32_t rem = len - body;
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
