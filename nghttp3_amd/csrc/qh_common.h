@@ -1,0 +1,226 @@
+// qh_common.h -- device-side types, tables and helpers shared by the
+// QPACK Huffman kernels (included once, from qh_device.hip).
+#pragma once
+
+namespace qhk {
+
+// ---------------------------------------------------------------------------
+// device-side types and helpers
+// ---------------------------------------------------------------------------
+
+struct SpanIn {
+  uint64_t off;
+  uint32_t len;
+  uint32_t flags;
+};
+struct SpanOut {
+  uint64_t off;
+  uint32_t len;
+  int32_t status;
+};
+static_assert(sizeof(SpanIn) == 16 && sizeof(qh_span_in) == 16, "span_in");
+static_assert(sizeof(SpanOut) == 16 && sizeof(qh_span_out) == 16, "span_out");
+
+// Device-side accumulators for qh_batch_stats (+ scan bookkeeping).
+struct DevStats {
+  unsigned long long n;
+  unsigned long long in_bytes;
+  unsigned long long out_bytes;
+  unsigned long long dst_bytes;
+  unsigned long long n_errors;
+  unsigned long long scan_timeouts;
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte vector with 1-byte alignment: gfx950 runs global_load_dwordx4 on
+// unaligned addresses (unaligned access mode), so a string can be fetched
+// from its own first byte without a head-alignment loop.
+typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+
+// Host images of the tables uploaded to every context (qh_tables.h lists).
+#define QH_SYM_PAIR(nbits, code) nbits, code,
+const uint32_t kSymPacked[QH_NSYM * 2] = {QH_SYM_LIST(QH_SYM_PAIR)};
+#define QH_FSM_WORD(w) w,
+#define QH_FSM_FLAT(...) __VA_ARGS__
+const uint32_t kFsmPacked[QH_NSTATE * 16] = {QH_FSM_ROWS(QH_FSM_FLAT, QH_FSM_WORD)};
+
+constexpr int kBlock = 256;
+constexpr uint32_t kFsmWords = QH_NSTATE * 16;  // 4112 words = 16,448 B
+constexpr uint32_t kFlagSymBit = 17;             // QH_FLAG_SYM << 16
+
+__device__ __forceinline__ uint32_t lds_word(const uint32_t *base,
+                                             uint32_t byte_off) {
+  return *reinterpret_cast<const uint32_t *>(
+      reinterpret_cast<const char *>(base) + byte_off);
+}
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Block-level sum of per-thread counters -> one atomic per block.
+__device__ __forceinline__ void block_add(unsigned long long *dst,
+                                          unsigned long long v,
+                                          unsigned long long *lds4) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds4[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += lds4[w];
+    if (s) atomicAdd(dst, s);
+  }
+  __syncthreads();
+}
+
+// Byte-exact output stream built from aligned dword stores.  The first and
+// the last partial dword of a string are written byte by byte so that
+// neighbouring strings (owned by other lanes) are never touched.
+struct Sink {
+  uint32_t *wp;      // current aligned dword
+  uint64_t acc;      // pending bytes, stream order = little-endian
+  uint32_t nb;       // pending bits (multiple of 8), includes head gap
+  uint32_t head;     // leading bytes of *wp that belong to someone else
+};
+
+// Pointer arithmetic (not integer casts) keeps the global address space, so
+// stores stay global_store_* rather than flat_* (flat ops also count on
+// lgkmcnt and would make every LDS lookup of the FSM wait for them).
+__device__ __forceinline__ void sink_init(Sink &s, uint8_t *p) {
+  s.head = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  s.wp = reinterpret_cast<uint32_t *>(p - s.head);
+  s.acc = 0;
+  s.nb = s.head * 8;
+}
+
+__device__ __forceinline__ void sink_flush(Sink &s) {  // needs nb >= 32
+  const uint32_t w = (uint32_t)s.acc;
+  if (s.head) {
+    uint8_t *b = reinterpret_cast<uint8_t *>(s.wp);
+    for (uint32_t k = s.head; k < 4; ++k) b[k] = (uint8_t)(w >> (8 * k));
+    s.head = 0;
+  } else {
+    *s.wp = w;
+  }
+  ++s.wp;
+  s.acc >>= 32;
+  s.nb -= 32;
+}
+
+__device__ __forceinline__ void sink_finish(Sink &s) {
+  const uint32_t nbytes = s.nb >> 3;
+  uint8_t *b = reinterpret_cast<uint8_t *>(s.wp);
+  for (uint32_t k = s.head; k < nbytes; ++k)
+    b[k] = (uint8_t)(s.acc >> (8 * k));
+}
+
+// Fetch the 16 bytes at p + pos where fewer than 16 may belong to the
+// string (tail): the last 16 bytes of the string are loaded and shifted so
+// that byte 0 of the result is byte `pos` of the string.  Strings shorter
+// than 16 bytes are gathered bytewise.  Bytes past the string are zero.
+__device__ __forceinline__ u32x4 load_tail(const uint8_t *p, uint32_t pos,
+                                           uint32_t len) {
+  const uint32_t rem = len - pos;  // 0 < rem < 16
+  u32x4 v = {0, 0, 0, 0};
+  if (len >= 16) {
+    const u32x4 w = *reinterpret_cast<const u32x4_ua *>(p + len - 16);
+    // move bytes [16 - rem, 16) of w down to [0, rem): 128-bit shift right
+    const uint32_t s = 8 * (16 - rem);  // 8..120 bits
+    const uint64_t lo64 = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    const uint64_t hi64 = (uint64_t)w.z | ((uint64_t)w.w << 32);
+    uint64_t rlo, rhi;
+    if (s >= 64) {
+      rlo = hi64 >> (s - 64);
+      rhi = 0;
+    } else {
+      rlo = (lo64 >> s) | (hi64 << (64 - s));
+      rhi = hi64 >> s;
+    }
+    v.x = (uint32_t)rlo; v.y = (uint32_t)(rlo >> 32);
+    v.z = (uint32_t)rhi; v.w = (uint32_t)(rhi >> 32);
+  } else {
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+      if (k < rem) o[k >> 2] |= (uint32_t)p[pos + k] << (8 * (k & 3));
+    v.x = o[0]; v.y = o[1]; v.z = o[2]; v.w = o[3];
+  }
+  return v;
+}
+
+// Plan of a batch (written by qh_k_plan; read by the tile kernels, which
+// run when bad == 0, and by the lane kernels, which run when bad != 0).
+struct PlanHdr {
+  uint32_t ntiles;
+  uint32_t bad;       // bit 0: spans not monotone, bit 1: too many tiles
+  uint32_t tile_ctr;  // dynamic tile ids (look-back needs claim order)
+  uint32_t pad;
+};
+
+// ---------------------------------------------------------------------------
+// decoupled look-back (single-pass prefix over tiles)
+// ---------------------------------------------------------------------------
+// A tile's state word is {flag:2, value:62}: 0 = nothing yet, A = the tile's
+// own aggregate, P = inclusive prefix through this tile.  Words are written
+// and polled with relaxed agent-scope atomics (one 8-byte granule carries
+// flag and value together, so no separate release is needed: the pattern of
+// MI355X_MICROARCH.md "R2").  Tile ids are drawn from an atomic counter, so
+// every predecessor of a waiting tile is already running.
+constexpr uint64_t kStA = 1ull << 62;
+constexpr uint64_t kStP = 2ull << 62;
+constexpr uint64_t kStMask = (1ull << 62) - 1;
+
+// Called by ALL 64 lanes of ONE wave; returns the exclusive prefix of `tile`
+// (identical in every lane) after publishing P for it.  `agg` must already
+// be published as A by the caller when tile > 0 (see publish_aggregate).
+__device__ __forceinline__ uint64_t lookback_wave(uint64_t *states,
+                                                  uint32_t tile, uint64_t agg,
+                                                  unsigned long long *timeouts) {
+  const int lane = threadIdx.x & 63;
+  uint64_t prefix = 0;
+  int64_t hi = (int64_t)tile - 1;  // next predecessor to inspect
+  uint32_t spins = 0;
+  while (hi >= 0) {
+    const int64_t j = hi - lane;
+    uint64_t v = j >= 0 ? ld_relaxed(&states[j]) : kStP;  // before tile 0: P(0)
+    const uint64_t flag = v & ~kStMask;
+    // lanes ordered nearest-first; find the nearest P and any gap before it
+    const unsigned long long pmask = __ballot(flag == kStP);
+    const unsigned long long xmask = __ballot(flag == 0);
+    const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
+    const unsigned long long before = first_p >= 64 ? ~0ull : ((2ull << first_p) - 1);
+    if (xmask & before) {  // a needed predecessor has not published yet
+      if (++spins > (1u << 24)) {
+        if (lane == 0) atomicAdd(timeouts, 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint64_t part = (lane <= first_p) ? (v & kStMask) : 0;
+    part = wave_sum(part);
+    prefix += part;
+    if (first_p < 64) break;
+    hi -= 64;
+  }
+  if (lane == 0) st_relaxed(&states[tile], kStP | (prefix + agg));
+  return prefix;
+}
+
+__device__ __forceinline__ void publish_aggregate(uint64_t *states,
+                                                  uint32_t tile, uint64_t agg) {
+  if (tile > 0) st_relaxed(&states[tile], kStA | agg);
+}
+
+}  // namespace qhk
