@@ -171,36 +171,60 @@ struct PlanHdr {
 // ---------------------------------------------------------------------------
 // decoupled look-back (single-pass prefix over tiles)
 // ---------------------------------------------------------------------------
-// A tile's state word is {flag:2, value:62}: 0 = nothing yet, A = the tile's
-// own aggregate, P = inclusive prefix through this tile.  Words are written
-// and polled with relaxed agent-scope atomics (one 8-byte granule carries
-// flag and value together, so no separate release is needed: the pattern of
-// MI355X_MICROARCH.md "R2").  Tile ids are drawn from an atomic counter, so
-// every predecessor of a waiting tile is already running.
+// Lane-path scan words: {flag:2, value:62}, zeroed by a memset per launch.
 constexpr uint64_t kStA = 1ull << 62;
 constexpr uint64_t kStP = 2ull << 62;
 constexpr uint64_t kStMask = (1ull << 62) - 1;
 
-// Called by ALL 64 lanes of ONE wave; returns the exclusive prefix of `tile`
-// (identical in every lane) after publishing P for it.  `agg` must already
-// be published as A by the caller when tile > 0 (see publish_aggregate).
+// Tile-engine words: {epoch:16, flag:2, value:46}.  A word whose epoch is
+// not the current launch's reads as "not published", so the words never
+// need zeroing and a value left by an earlier launch (in any XCD's cache) is
+// never mistaken for this launch's.  One 8-byte granule carries tag and value
+// together and is written and polled with relaxed agent-scope atomics (the
+// granule pattern of MI355X_MICROARCH.md), so no fences are needed.  Tile ids
+// come from an atomic counter, so every predecessor of a waiting tile is
+// already running and the wait ends.
+constexpr uint64_t kTagA = 1ull << 46;
+constexpr uint64_t kTagP = 2ull << 46;
+constexpr uint64_t kTagValMask = (1ull << 46) - 1;
+
+__device__ __forceinline__ uint64_t tag_word(uint32_t epoch, uint64_t flag,
+                                             uint64_t value) {
+  return ((uint64_t)epoch << 48) | flag | value;
+}
+
+__device__ __forceinline__ void publish_aggregate(uint64_t *states,
+                                                  uint32_t tile, uint64_t agg,
+                                                  uint32_t epoch) {
+  if (tile > 0) st_relaxed(&states[tile], tag_word(epoch, kTagA, agg));
+}
+
+// Called by ALL 64 lanes of ONE wave; returns the exclusive prefix of
+// `tile` (same in every lane) and publishes P for it.  The caller has
+// published A for tile > 0 (publish_aggregate).
 __device__ __forceinline__ uint64_t lookback_wave(uint64_t *states,
                                                   uint32_t tile, uint64_t agg,
+                                                  uint32_t epoch,
                                                   unsigned long long *timeouts) {
   const int lane = threadIdx.x & 63;
   uint64_t prefix = 0;
-  int64_t hi = (int64_t)tile - 1;  // next predecessor to inspect
+  int64_t hi = (int64_t)tile - 1;  // nearest predecessor not yet summed
   uint32_t spins = 0;
   while (hi >= 0) {
-    const int64_t j = hi - lane;
-    uint64_t v = j >= 0 ? ld_relaxed(&states[j]) : kStP;  // before tile 0: P(0)
-    const uint64_t flag = v & ~kStMask;
-    // lanes ordered nearest-first; find the nearest P and any gap before it
-    const unsigned long long pmask = __ballot(flag == kStP);
+    const int64_t j = hi - lane;  // lane 0 = nearest
+    uint64_t flag = kTagP, val = 0;  // before tile 0: P(0)
+    if (j >= 0) {
+      const uint64_t w = ld_relaxed(&states[j]);
+      const bool cur = (uint32_t)(w >> 48) == epoch;
+      flag = cur ? (w & (3ull << 46)) : 0;
+      val = w & kTagValMask;
+    }
+    const unsigned long long pmask = __ballot(flag == kTagP);
     const unsigned long long xmask = __ballot(flag == 0);
     const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
-    const unsigned long long before = first_p >= 64 ? ~0ull : ((2ull << first_p) - 1);
-    if (xmask & before) {  // a needed predecessor has not published yet
+    const unsigned long long need =
+        first_p >= 63 ? ~0ull : ((2ull << first_p) - 1);
+    if (xmask & need) {  // a predecessor we need has not published yet
       if (++spins > (1u << 24)) {
         if (lane == 0) atomicAdd(timeouts, 1ull);
         break;
@@ -208,19 +232,12 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t *states,
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    uint64_t part = (lane <= first_p) ? (v & kStMask) : 0;
-    part = wave_sum(part);
-    prefix += part;
+    prefix += wave_sum(lane <= first_p ? val : 0ull);
     if (first_p < 64) break;
     hi -= 64;
   }
-  if (lane == 0) st_relaxed(&states[tile], kStP | (prefix + agg));
+  if (lane == 0) st_relaxed(&states[tile], tag_word(epoch, kTagP, prefix + agg));
   return prefix;
-}
-
-__device__ __forceinline__ void publish_aggregate(uint64_t *states,
-                                                  uint32_t tile, uint64_t agg) {
-  if (tile > 0) st_relaxed(&states[tile], kStA | agg);
 }
 
 }  // namespace qhk

@@ -234,3 +234,35 @@ def test_full_size_config(codec, digests, name):
     rep_p = torch.repeat_interleave(poff, ln)
     pos = torch.arange(total, device="cuda", dtype=torch.int64) - rep_p
     assert bool((dec[rep_d + pos] == src[:total]).all())
+
+
+def test_encode_unordered_spans_fallback(codec, corpus):
+    # non-monotone spans take the lane-per-string kernels; same bytes
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    rng = np.random.default_rng(5)
+    idx = rng.permutation(len(ln))[:2000]
+    enc, o, l, s = encode_dev(codec, plain, off[idx], ln[idx])
+    assert (s == 0).all()
+    for j, i in enumerate(idx):
+        want = oracle.encode(plain[off[i]:off[i] + ln[i]].tobytes())
+        assert enc[o[j]:o[j] + l[j]].tobytes() == want
+
+
+def test_encode_gapped_spans_tiles(codec, corpus):
+    # monotone spans with gaps between strings (header-block framing bytes)
+    # stay on the tile engine
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    rng = np.random.default_rng(6)
+    gaps = rng.integers(0, 9, len(ln))
+    buf = bytearray()
+    offs = []
+    for i in range(len(ln)):
+        buf += bytes(rng.integers(0, 256, gaps[i]).astype(np.uint8))
+        offs.append(len(buf))
+        buf += plain[off[i]:off[i] + ln[i]].tobytes()
+    src = np.frombuffer(bytes(buf), dtype=np.uint8)
+    enc, o, l, s = encode_dev(codec, src, np.array(offs), ln)
+    assert (s == 0).all()
+    total = int(corpus["enc_len"].astype(np.int64).sum())
+    assert (l == corpus["enc_len"].astype(np.int64)).all()
+    assert (enc[:total] == corpus["enc"]).all()
