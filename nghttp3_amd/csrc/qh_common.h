@@ -164,8 +164,8 @@ __device__ __forceinline__ u32x4 load_tail(const uint8_t *p, uint32_t pos,
 struct PlanHdr {
   uint32_t ntiles;
   uint32_t bad;       // bit 0: spans not monotone, bit 1: too many tiles
-  uint32_t tile_ctr;  // dynamic tile ids (look-back needs claim order)
-  uint32_t pad;
+  uint32_t ctr_a;     // tile claim counter of the first pass
+  uint32_t ctr_b;     // tile claim counter of the second pass
 };
 
 // ---------------------------------------------------------------------------

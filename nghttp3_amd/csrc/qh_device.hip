@@ -38,7 +38,8 @@
 // One translation unit, split by concern:
 #include "qh_common.h"   // span/stat types, tables, LDS + scan helpers
 #include "qh_lane.inc"   // lane-per-string kernels (general spans)
-#include "qh_tile.inc"   // tile engine: coalesced I/O, look-back offsets
+#include "qh_tile.inc"      // tile engine: plan, shared helpers
+#include "qh_tile_enc.inc"  // tile encoder (count / scan / emit)
 #include "qh_synth.inc"  // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
 
