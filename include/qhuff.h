@@ -160,15 +160,17 @@ QH_EXPORT int qh_ctx_sync(qh_ctx *ctx);
 /* Totals of the last batch call (synchronises the stream). */
 QH_EXPORT int qh_ctx_last_stats(qh_ctx *ctx, qh_batch_stats *stats);
 
-/* Destination sizing.  Decode follows the reference's ownership convention:
- * string i owns a slot sized by nghttp3_qpack_huffman_estimate_decode_length
- * (the rcbuf the reference allocates at qpack.c:2977,3065,3591,3677, minus
- * the NUL), rounded up to 16 bytes so every slot starts 16-byte aligned:
- *   slot(len) = round_up(len * 8 / 5, 16),
- * slots back to back in string order, out[i].off = sum_{j<i} slot(in[j].len),
- * dst_cap >= qh_decode_dst_size(in, n).  Bytes of a slot past out[i].len are
- * unspecified.  Encode output is dense: out[i].off = sum_{j<i}
- * encode_count(string j); qh_encode_dst_bound() is an upper bound. */
+/* Destination sizing.  A decoded string never exceeds the reference's
+ * estimate_decode_length(len) = len * 8 / 5 (huffman.h:113-115; the caller
+ * of the reference sizes its rcbuf from it, qpack.c:2977,3065,3591,3677).
+ * qh_decode_dst_size(in, n) = sum of round_up(len * 8 / 5, 16) is enough
+ * for any batch.  Decoded strings are placed in string order without
+ * overlap inside [0, that size); consecutive strings are packed densely
+ * (monotone spans) or start on 16-byte boundaries (other spans), and
+ * out[i].off / out[i].len say where each one is.  A group of strings that
+ * does not fit in dst_cap gets QH_ERR_NOMEM and nothing is written for it.
+ * Encode output is dense: out[i].off = sum_{j<i} encode_count(string j);
+ * qh_encode_dst_bound() is an upper bound. */
 QH_EXPORT uint64_t qh_decode_dst_size(const qh_span_in *in, size_t n);
 QH_EXPORT uint64_t qh_encode_dst_bound(const qh_span_in *in, size_t n);
 

@@ -38,6 +38,16 @@ def spans_dev(off, ln):
     return to_dev(sp)
 
 
+def assert_disjoint(o, l, cap):
+    """Output spans lie inside [0, cap) and do not overlap (any order)."""
+    o = np.asarray(o, dtype=np.int64)
+    l = np.asarray(l, dtype=np.int64)
+    assert (o >= 0).all() and (o + l <= cap).all()
+    idx = np.argsort(o, kind="stable")
+    so, sl = o[idx], l[idx]
+    assert (so[1:] >= so[:-1] + sl[:-1]).all()
+
+
 def decode_dev(codec, enc, off, ln, cap=None):
     torch = torch_mod()
     n = len(ln)
@@ -82,8 +92,8 @@ def test_corpus_decode(codec, corpus):
     want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
     dst, o, l, s = decode_dev(codec, enc, eoff, elen)
     assert (s == 0).all()
-    assert (o == want_slot.astype(np.int64)).all()
     assert (l == want_len.astype(np.int64)).all()
+    assert_disjoint(o, l, int(q.decode_slot_size(elen.astype(np.int64)).sum()))
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
     for i in range(len(ln)):
         assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes(), i
@@ -157,14 +167,20 @@ def test_unordered_overlapping_spans(codec, corpus):
 
 
 def test_dst_cap_too_small(codec, corpus):
+    # Strings whose group of output does not fit get QH_ERR_NOMEM and write
+    # nothing; every other string is decoded correctly inside dst_cap.
     enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
-    n = 300
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    n = 3000
     slots = q.decode_slot_size(elen[:n].astype(np.int64))
-    cap = int(slots[:150].sum())
+    cap = int(slots.sum()) // 3
     dst, o, l, s = decode_dev(codec, enc, eoff[:n], elen[:n], cap=cap)
-    fits = (o + slots) <= cap
-    assert (s[fits] == 0).all()
-    assert (s[~fits] == q.QH_ERR_NOMEM).all()
+    assert set(np.unique(s)) <= {0, q.QH_ERR_NOMEM}
+    assert (s == 0).any() and (s == q.QH_ERR_NOMEM).any()
+    ok = s == 0
+    assert_disjoint(o[ok], l[ok], cap)
+    for i in np.nonzero(ok)[0]:
+        assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes()
 
 
 def test_host_path_matches(codec, corpus):
@@ -174,8 +190,10 @@ def test_host_path_matches(codec, corpus):
     dst, out = codec.decode_host(enc, sp)
     want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
     assert (out["status"] == 0).all() and (out["len"] == want_len).all()
-    assert (out["off"] == want_slot).all()
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    for i in range(0, len(ln), 7):
+        o, n_ = int(out["off"][i]), int(out["len"][i])
+        assert dst[o:o + n_].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes()
     psp = np.zeros(len(ln), dtype=q.SPAN_IN_DTYPE)
     psp["off"], psp["len"] = off, ln
     e2, eout = codec.encode_host(plain, psp)
