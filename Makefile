@@ -21,12 +21,20 @@ $(LIBDIR)/qh_scalar.o: $(CSRC)/qh_scalar.c $(CSRC)/qh_tables.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/qh_tables.h include/qhuff.h
+$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(CSRC)/qh_tables.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# Phase-timer build for kernel development (not loaded unless QHUFF_LIB
+# points at it).
+STAMPS := $(LIBDIR)/libqhuff_stamps.so
+stamps: $(STAMPS)
+$(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o
+	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -c $< -o $(LIBDIR)/qh_device_stamps.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_stamps.o $(LIBDIR)/qh_scalar.o
 
 # Oracle: -O2 -mavx2 as nghttp3's README.rst:61-67 prescribes for the
 # reference build (the Huffman loop itself has no SIMD path).
@@ -34,6 +42,6 @@ $(ORACLE): oracle/qh_oracle.c oracle/qh_oracle.h
 	$(CC) -std=c11 -O2 -mavx2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIB) $(ORACLE)
+	rm -f $(LIBDIR)/*.o $(LIB) $(STAMPS) $(ORACLE)
 
-.PHONY: all clean
+.PHONY: all clean stamps

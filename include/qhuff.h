@@ -163,12 +163,12 @@ QH_EXPORT int qh_ctx_last_stats(qh_ctx *ctx, qh_batch_stats *stats);
 /* Destination sizing.  A decoded string never exceeds the reference's
  * estimate_decode_length(len) = len * 8 / 5 (huffman.h:113-115; the caller
  * of the reference sizes its rcbuf from it, qpack.c:2977,3065,3591,3677).
- * qh_decode_dst_size(in, n) = sum of round_up(len * 8 / 5, 16) is enough
- * for any batch.  Decoded strings are placed in string order without
- * overlap inside [0, that size); consecutive strings are packed densely
- * (monotone spans) or start on 16-byte boundaries (other spans), and
- * out[i].off / out[i].len say where each one is.  A group of strings that
- * does not fit in dst_cap gets QH_ERR_NOMEM and nothing is written for it.
+ * Batch decode gives string i a slot of len_i * 8 / 5 + 16 bytes, slots in
+ * string order and back to back, so qh_decode_dst_size(in, n) = sum of
+ * (len * 8 / 5 + 16) is what a batch needs; out[i].off is the start of the
+ * slot and out[i].len the decoded length.  The other bytes of a slot are
+ * unspecified.  A string whose slot does not fit in dst_cap gets
+ * QH_ERR_NOMEM; nothing is written at or past dst_cap.
  * Encode output is dense: out[i].off = sum_{j<i} encode_count(string j);
  * qh_encode_dst_bound() is an upper bound. */
 QH_EXPORT uint64_t qh_decode_dst_size(const qh_span_in *in, size_t n);

@@ -11,6 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libqhuff.so")
+# Development builds (e.g. the phase-timer library of `make stamps`) are
+# selected with QHUFF_LIB; there is no fallback to anything else.
+LIB_PATH = os.environ.get("QHUFF_LIB", LIB_PATH)
 
 QH_OK = 0
 QH_ERR_INVALID_ARGUMENT = -101

@@ -4,6 +4,31 @@
 
 namespace qhk {
 
+// Phase timers for kernel development (make stamps -> libqhuff_stamps.so):
+// wave 0 of every workgroup adds s_memtime deltas per phase slot.  Compiled
+// out of the product library.
+#ifdef QH_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define QH_ST_INIT()                                                         \
+  unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_a[16] = {0};
+#define QH_ST(k)                                                             \
+  {                                                                          \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();             \
+    _st_a[k] += _n - _st_t;                                                  \
+    _st_t = _n;                                                              \
+  }
+#define QH_ST_COUNT(k, v) (_st_a[k] += (v))
+#define QH_ST_FLUSH()                                                        \
+  if (threadIdx.x == 0)                                                      \
+    for (int _k = 0; _k < 16; ++_k)                                          \
+      if (_st_a[_k]) atomicAdd(&g_stamps[_k], _st_a[_k]);
+#else
+#define QH_ST_INIT()
+#define QH_ST(k)
+#define QH_ST_COUNT(k, v)
+#define QH_ST_FLUSH()
+#endif
+
 // ---------------------------------------------------------------------------
 // device-side types and helpers
 // ---------------------------------------------------------------------------

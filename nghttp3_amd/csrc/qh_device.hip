@@ -40,7 +40,9 @@
 #include "qh_lane.inc"   // lane-per-string kernels (general spans)
 #include "qh_tile.inc"      // tile engine: plan, shared helpers
 #include "qh_tile_enc.inc"  // tile encoder (count / scan / emit)
-#include "qh_tile_dec.inc"  // tile decoder (capacity / scan / decode)
+#include "qh_chunk.inc"     // chunk engine: block ranges, windows, rounds
+#include "qh_chunk_dec.inc"  // chunk decoder (reserve / decode)
+#include "qh_lane_dec.inc"   // lane-per-string decoder
 #include "qh_synth.inc"  // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
 

@@ -1,0 +1,76 @@
+"""Per-phase cycle breakdown of the tile kernels (development tool).
+
+Run with QHUFF_LIB=nghttp3_amd/lib/libqhuff_stamps.so (built by
+`make stamps`).  Prints, per kernel, the wave-0 cycles per tile and per
+round for each phase slot (see QH_ST(k) in the kernels).
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nghttp3_amd import HuffmanBatchCodec, _lib  # noqa: E402
+from nghttp3_amd.qpack_huffman import decode_slot_size  # noqa: E402
+from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
+
+# kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
+LAYOUT = {
+    "enc_count": ({11: "setup", 12: "rounds", 13: "lens+scan"}, 14, 15, None),
+    "enc_emit": ({0: "setup", 1: "load+cb", 2: "carry_scan", 3: "emit", 4: "copy"}, 9, 10, None),
+    "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
+    "dec_chunks": ({0: "window", 1: "map+load", 2: "pass1", 3: "fixup", 4: "scan+pass2",
+                    5: "copy", 6: "results"}, 9, 10, 8),
+}
+
+
+def main():
+    lib = _lib.load()
+    assert "stamps" in _lib.LIB_PATH, "set QHUFF_LIB to the stamps build"
+    lib.qh_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    buf = (ctypes.c_uint64 * 16)()
+
+    def read():
+        assert lib.qh_debug_stamps(buf, 1) == 0
+        return list(buf)
+
+    n = int(os.environ.get("N", 1 << 20))
+    codec = HuffmanBatchCodec(0)
+    dev = torch.device("cuda", 0)
+    src, spans, total = codec.synth(0x5EED0003, n, 8, 256, ALPHABET_A)
+    enc = torch.empty(total * 4 + 64, dtype=torch.uint8, device=dev)
+    eout = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    dout = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    hlen = torch.empty(n, dtype=torch.int32, device=dev)
+    codec.encode_dev(src, spans, enc, eout)
+    codec.sync()
+    cap = int(decode_slot_size((eout[:, 1] & 0xFFFFFFFF).cpu().numpy()).sum())
+    dec = torch.empty(cap + 64, dtype=torch.uint8, device=dev)
+    codec.decode_dev(enc, eout, dec, dout)
+    codec.sync()
+    read()
+    reps = 5
+    runs = {
+        "enc_count": lambda: codec.encode_count_dev(src, spans, hlen),
+        "enc_emit": lambda: codec.encode_dev(src, spans, enc, eout),
+        "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
+    }
+    for kern, fn in runs.items():
+        for _ in range(reps):
+            fn()
+        codec.sync()
+        st = read()
+        phases, rs, ts, xs = LAYOUT[kern]
+        rounds, tiles = max(st[rs], 1), max(st[ts], 1)
+        extra = f" counter/round={st[xs] / rounds:.2f}" if xs is not None else ""
+        print(f"{kern}: windows/launch={tiles / reps:.0f} rounds/launch={rounds / reps:.0f}{extra}")
+        tot = sum(st[k] for k in phases)
+        for k, nm in phases.items():
+            print(f"  {nm:11s} {st[k] / tiles:9.0f} cyc/tile {st[k] / rounds:8.0f} cyc/round"
+                  f"  {100 * st[k] / max(tot, 1):5.1f}%")
+        print(f"  wave0 cycles/launch {tot / reps:.3e}")
+
+
+if __name__ == "__main__":
+    main()
