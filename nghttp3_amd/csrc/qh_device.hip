@@ -42,7 +42,8 @@
 #include "qh_tile_enc.inc"  // tile encoder (count / scan / emit)
 #include "qh_chunk.inc"     // chunk engine: block ranges, windows, rounds
 #include "qh_chunk_dec.inc"  // chunk decoder (reserve / decode)
-#include "qh_lane_dec.inc"   // lane-per-string decoder
+#include "qh_lane_dec.inc"   // lane-per-string decoder (4-bit FSM)
+#include "qh_lut_dec.inc"    // lane-per-string decoder (12-bit table)
 #include "qh_synth.inc"  // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
 

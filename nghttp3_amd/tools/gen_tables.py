@@ -165,6 +165,78 @@ def packed_fsm():
     return [[f | (fl << 16) | (s << 24) for f, fl, s in row] for row in decode_fsm()]
 
 
+# ---------------------------------------------------------------------------
+# Symbol-level decode tables (the batch decoder, qh_lane_dec.inc).  They are a
+# different *layout* of the same code: canonical_codes() is their only input,
+# and tests/test_lut_model.py checks a model of the decoder that uses them
+# against the oracle.
+# ---------------------------------------------------------------------------
+
+LUT_BITS = 12
+
+
+def lut12():
+    """4096 words indexed by the next 12 bits of input (MSB first).
+
+    word = consumed | nsym << 8 | sym1 << 16 | sym2 << 24, where the window
+    starts with sym1's code and, if it also fits, sym2's code (consumed = the
+    bits of both).  nsym = 0 (word 0) marks the 4 windows that start a code
+    longer than 12 bits (all such codes begin with ten 1-bits)."""
+    dec = {}
+    for s, (n, c) in enumerate(canonical_codes()):
+        if n <= LUT_BITS:
+            dec[(n, c)] = s
+
+    def first(bits, avail):  # bits: `avail`-bit integer, MSB first
+        for n in range(1, avail + 1):
+            s = dec.get((n, bits >> (avail - n)))
+            if s is not None:
+                return s, n
+        return None
+
+    out = []
+    for i in range(1 << LUT_BITS):
+        r1 = first(i, LUT_BITS)
+        if r1 is None:
+            out.append(0)
+            continue
+        s1, n1 = r1
+        rest = LUT_BITS - n1
+        r2 = first(i & ((1 << rest) - 1), rest) if rest else None
+        if r2 is None:
+            out.append(n1 | 1 << 8 | s1 << 16)
+        else:
+            s2, n2 = r2
+            out.append((n1 + n2) | 2 << 8 | s1 << 16 | s2 << 24)
+    return out
+
+
+def canonical_slow():
+    """Canonical decoding of any code from a left-aligned 32-bit window w.
+
+    Returns (lengths, lim, first_aligned, rank, lsym): for the k-th present
+    code length L = lengths[k], lim[k] = (last code of length L + 1) <<
+    (32 - L) (exclusive upper bound of those codes, left-aligned; the last
+    one is 2**32), first_aligned[k] = first code << (32 - L), rank[k] = number
+    of symbols with shorter codes, and lsym = symbols in canonical order.
+    Decoding: k = #{j : w >= lim[j]}; L = lengths[k];
+    sym = lsym[rank[k] + ((w - first_aligned[k]) >> (32 - L))]."""
+    codes = canonical_codes()
+    lengths = sorted(set(n for n, _ in codes))
+    lsym = sorted(range(len(codes)), key=lambda s: (codes[s][0], s))
+    lim, fa, rank = [], [], []
+    r = 0
+    for L in lengths:
+        syms = [s for s in lsym if codes[s][0] == L]
+        cs = [codes[s][1] for s in syms]
+        assert cs == list(range(cs[0], cs[0] + len(cs)))
+        fa.append(cs[0] << (32 - L))
+        lim.append((cs[-1] + 1) << (32 - L))
+        rank.append(r)
+        r += len(syms)
+    return lengths, lim, fa, rank, lsym
+
+
 def render_header():
     out = []
     w = out.append
@@ -201,6 +273,29 @@ def render_header():
         items = ["X(0x%08Xu)" % x for x in row]
         w("  R(" + " ".join(items[:8]) + " \\")
         w("    " + " ".join(items[8:]) + ") \\")
+    w("")
+    w("")
+    w("/* Symbol-level decode tables (gen_tables.py lut12 / canonical_slow):")
+    w(" *   QH_LUT12_LIST(X)  X(word) for the 4096 12-bit windows;")
+    w(" *   QH_SLOW_LIST(X)   X(lim, first_aligned, length, rank) per present")
+    w(" *                     code length, shortest first (lim of the last = 0,")
+    w(" *                     i.e. 2**32 truncated: never compared);")
+    w(" *   QH_LSYM_LIST(X)   X(sym) for the 257 symbols in canonical order. */")
+    w("#define QH_LUT12_BITS %d" % LUT_BITS)
+    w("#define QH_LUT12_LIST(X) \\")
+    lut = lut12()
+    for i in range(0, len(lut), 8):
+        w("  " + " ".join("X(0x%08Xu)" % x for x in lut[i:i + 8]) + " \\")
+    w("")
+    lengths, lim, fa, rank, lsym = canonical_slow()
+    w("#define QH_SLOW_NLEN %d" % len(lengths))
+    w("#define QH_SLOW_LIST(X) \\")
+    for k in range(len(lengths)):
+        w("  X(0x%08Xu, 0x%08Xu, %d, %d) \\" % (lim[k] & 0xFFFFFFFF, fa[k], lengths[k], rank[k]))
+    w("")
+    w("#define QH_LSYM_LIST(X) \\")
+    for i in range(0, len(lsym), 16):
+        w("  " + " ".join("X(%d)" % x for x in lsym[i:i + 16]) + " \\")
     w("")
     w("")
     w("#endif /* QH_TABLES_H */")

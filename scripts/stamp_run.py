@@ -56,7 +56,10 @@ def main():
         "enc_emit": lambda: codec.encode_dev(src, spans, enc, eout),
         "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
     }
+    only = os.environ.get("KERNELS")
     for kern, fn in runs.items():
+        if only and kern not in only.split(","):
+            continue
         for _ in range(reps):
             fn()
         codec.sync()
