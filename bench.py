@@ -157,12 +157,13 @@ def main():
     value = total_all * args.steps / elapsed_max / GIB
 
     # roofline: dominant kernel by time; algorithmic bytes per launch
-    algo = {
-        "qh_k_decode": enc_bytes + total + 32 * n,       # E + D + 16 B in + 16 B out span
-        "qh_k_encode": total + enc_bytes + 32 * n,       # D + E + spans
-        "qh_k_count": total + 16 * n + 8 * n,            # D + in span + out len/status
-        "qh_k_scan_slots": 16 * n + 8 * n,
-        "qh_k_scan_hlen": 16 * n + 8 * n,
+    algo = {  # algorithmic HBM bytes per launch (DESIGN.md "Roofline")
+        "qh_k_dec_lanes": enc_bytes + total + 32 * n,    # E + D + 16 B span in + 16 B out
+        "qh_k_dec_lut": enc_bytes + total + 32 * n,
+        "qh_k_dec_reserve": 16 * n,                      # spans in
+        "qh_k_enc_lens": total + 16 * n + 8 * n,         # D + spans in + len/status out
+        "qh_k_enc_lanes": total + enc_bytes + 16 * n + 8 * n + 16 * n,  # D + E + spans
+        "qh_k_scan": 24 * n,
     }
     kern = {}
     for name, (cnt, ms) in ktimes.items():

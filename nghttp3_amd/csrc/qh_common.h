@@ -109,47 +109,6 @@ __device__ __forceinline__ void block_add(unsigned long long *dst,
   __syncthreads();
 }
 
-// Byte-exact output stream built from aligned dword stores.  The first and
-// the last partial dword of a string are written byte by byte so that
-// neighbouring strings (owned by other lanes) are never touched.
-struct Sink {
-  uint32_t *wp;      // current aligned dword
-  uint64_t acc;      // pending bytes, stream order = little-endian
-  uint32_t nb;       // pending bits (multiple of 8), includes head gap
-  uint32_t head;     // leading bytes of *wp that belong to someone else
-};
-
-// Pointer arithmetic (not integer casts) keeps the global address space, so
-// stores stay global_store_* rather than flat_* (flat ops also count on
-// lgkmcnt and would make every LDS lookup of the FSM wait for them).
-__device__ __forceinline__ void sink_init(Sink &s, uint8_t *p) {
-  s.head = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-  s.wp = reinterpret_cast<uint32_t *>(p - s.head);
-  s.acc = 0;
-  s.nb = s.head * 8;
-}
-
-__device__ __forceinline__ void sink_flush(Sink &s) {  // needs nb >= 32
-  const uint32_t w = (uint32_t)s.acc;
-  if (s.head) {
-    uint8_t *b = reinterpret_cast<uint8_t *>(s.wp);
-    for (uint32_t k = s.head; k < 4; ++k) b[k] = (uint8_t)(w >> (8 * k));
-    s.head = 0;
-  } else {
-    *s.wp = w;
-  }
-  ++s.wp;
-  s.acc >>= 32;
-  s.nb -= 32;
-}
-
-__device__ __forceinline__ void sink_finish(Sink &s) {
-  const uint32_t nbytes = s.nb >> 3;
-  uint8_t *b = reinterpret_cast<uint8_t *>(s.wp);
-  for (uint32_t k = s.head; k < nbytes; ++k)
-    b[k] = (uint8_t)(s.acc >> (8 * k));
-}
-
 // Fetch the 16 bytes at p + pos where fewer than 16 may belong to the
 // string (tail): the last 16 bytes of the string are loaded and shifted so
 // that byte 0 of the result is byte `pos` of the string.  Strings shorter
@@ -184,15 +143,6 @@ __device__ __forceinline__ u32x4 load_tail(const uint8_t *p, uint32_t pos,
   return v;
 }
 
-// Plan of a batch (written by qh_k_plan; read by the tile kernels, which
-// run when bad == 0, and by the lane kernels, which run when bad != 0).
-struct PlanHdr {
-  uint32_t ntiles;
-  uint32_t bad;       // bit 0: spans not monotone, bit 1: too many tiles
-  uint32_t ctr_a;     // tile claim counter of the first pass
-  uint32_t ctr_b;     // tile claim counter of the second pass
-};
-
 // ---------------------------------------------------------------------------
 // decoupled look-back (single-pass prefix over tiles)
 // ---------------------------------------------------------------------------
@@ -201,68 +151,18 @@ constexpr uint64_t kStA = 1ull << 62;
 constexpr uint64_t kStP = 2ull << 62;
 constexpr uint64_t kStMask = (1ull << 62) - 1;
 
-// Tile-engine words: {epoch:16, flag:2, value:46}.  A word whose epoch is
-// not the current launch's reads as "not published", so the words never
-// need zeroing and a value left by an earlier launch (in any XCD's cache) is
-// never mistaken for this launch's.  One 8-byte granule carries tag and value
-// together and is written and polled with relaxed agent-scope atomics (the
-// granule pattern of MI355X_MICROARCH.md), so no fences are needed.  Tile ids
-// come from an atomic counter, so every predecessor of a waiting tile is
-// already running and the wait ends.
-constexpr uint64_t kTagA = 1ull << 46;
-constexpr uint64_t kTagP = 2ull << 46;
-constexpr uint64_t kTagValMask = (1ull << 46) - 1;
-
-__device__ __forceinline__ uint64_t tag_word(uint32_t epoch, uint64_t flag,
-                                             uint64_t value) {
-  return ((uint64_t)epoch << 48) | flag | value;
+// Output slot of a string of `len` encoded bytes in a batch decode
+// (include/qhuff.h): the reference's estimate_decode_length
+// (huffman.h:113-115) + 16 spare bytes.
+__host__ __device__ __forceinline__ uint64_t qh_dec_slot(uint32_t len) {
+  return (uint64_t)len * 8 / 5 + 16;
 }
 
-__device__ __forceinline__ void publish_aggregate(uint64_t *states,
-                                                  uint32_t tile, uint64_t agg,
-                                                  uint32_t epoch) {
-  if (tile > 0) st_relaxed(&states[tile], tag_word(epoch, kTagA, agg));
-}
-
-// Called by ALL 64 lanes of ONE wave; returns the exclusive prefix of
-// `tile` (same in every lane) and publishes P for it.  The caller has
-// published A for tile > 0 (publish_aggregate).
-__device__ __forceinline__ uint64_t lookback_wave(uint64_t *states,
-                                                  uint32_t tile, uint64_t agg,
-                                                  uint32_t epoch,
-                                                  unsigned long long *timeouts) {
-  const int lane = threadIdx.x & 63;
-  uint64_t prefix = 0;
-  int64_t hi = (int64_t)tile - 1;  // nearest predecessor not yet summed
-  uint32_t spins = 0;
-  while (hi >= 0) {
-    const int64_t j = hi - lane;  // lane 0 = nearest
-    uint64_t flag = kTagP, val = 0;  // before tile 0: P(0)
-    if (j >= 0) {
-      const uint64_t w = ld_relaxed(&states[j]);
-      const bool cur = (uint32_t)(w >> 48) == epoch;
-      flag = cur ? (w & (3ull << 46)) : 0;
-      val = w & kTagValMask;
-    }
-    const unsigned long long pmask = __ballot(flag == kTagP);
-    const unsigned long long xmask = __ballot(flag == 0);
-    const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
-    const unsigned long long need =
-        first_p >= 63 ? ~0ull : ((2ull << first_p) - 1);
-    if (xmask & need) {  // a predecessor we need has not published yet
-      if (++spins > (1u << 24)) {
-        if (lane == 0) atomicAdd(timeouts, 1ull);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    prefix += wave_sum(lane <= first_p ? val : 0ull);
-    if (first_p < 64) break;
-    hi -= 64;
-  }
-  if (lane == 0) st_relaxed(&states[tile], tag_word(epoch, kTagP, prefix + agg));
-  return prefix;
-}
+// LDS image of the decode FSM (qh_lane_dec.inc): rows padded to 17 dwords so
+// that entry (row r, nibble v) lies in bank (17 r + v) mod 32 -- with
+// 16-dword rows every lane reading nibble v would hit one of two banks, and
+// header text has a few dominant high nibbles (0x4-0x7).
+constexpr uint32_t kFsmRowWords = 17;
+constexpr uint32_t kFsmLdsWords = QH_NSTATE * kFsmRowWords;  // 17,476 B
 
 }  // namespace qhk
