@@ -1,57 +1,79 @@
-// Dependent LDS lookup chain latency vs occupancy / chains per lane
-// (development microbenchmark; not part of the product).
+// Dependent LDS lookup chain: latency and throughput vs occupancy and chains
+// per lane (development microbenchmark; not part of the product).
+// Table: FSM-shaped, 257 rows x 16 dwords, entry = next_row_offset << 16.
+// Nibble source: a per-chain register rotated by 4 bits per step (one
+// v_alignbit), so the loop is LDS-bound, not VALU-bound.
 #include <hip/hip_runtime.h>
-#include <stdio.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <vector>
 
-template <int CHAINS>
-__global__ __launch_bounds__(256) void chain(const uint32_t *g, uint32_t *out, int steps, int pad_rows) {
-  extern __shared__ uint32_t tab[];  // 257*16 words + padding (occupancy knob)
+template <int CHAINS, bool STORE>
+__global__ __launch_bounds__(256) void chain(const uint32_t *g, uint32_t *out, int steps) {
+  extern __shared__ uint32_t tab[];  // 257*16 words + ring + padding
   for (int i = threadIdx.x; i < 257 * 16; i += 256) tab[i] = g[i];
   __syncthreads();
-  uint32_t e[CHAINS], x[CHAINS];
+  uint8_t *ring = reinterpret_cast<uint8_t *>(tab + 257 * 16) + threadIdx.x * 48;
+  uint32_t e[CHAINS], x[CHAINS], k = 0;
 #pragma unroll
-  for (int c = 0; c < CHAINS; ++c) { e[c] = 0; x[c] = threadIdx.x * 2654435761u + c * 97 + blockIdx.x; }
+  for (int c = 0; c < CHAINS; ++c) {
+    e[c] = 0;
+    x[c] = (threadIdx.x * 2654435761u) ^ (c * 0x9E3779B9u) ^ (blockIdx.x * 40503u);
+  }
   for (int s = 0; s < steps; ++s) {
 #pragma unroll
     for (int c = 0; c < CHAINS; ++c) {
-      x[c] = x[c] * 1664525u + 1013904223u;
-      const uint32_t nib = (x[c] >> 26) << 2;  // nibble * 4
+      x[c] = __builtin_amdgcn_alignbit(x[c], x[c], 4);  // rotate by 4
+      const uint32_t nib = x[c] & 0x3Cu;
       e[c] = *(const uint32_t *)((const char *)tab + (e[c] >> 16) + nib);
+      if (STORE) {
+        ring[k & 31] = (uint8_t)e[c];
+        k += (e[c] >> 8) & 1u;
+      }
     }
   }
-  uint32_t r = 0;
+  uint32_t r = k;
 #pragma unroll
   for (int c = 0; c < CHAINS; ++c) r += e[c];
   out[blockIdx.x * 256 + threadIdx.x] = r;
 }
 
 int main() {
-  // random FSM-like table: entry = next_row_offset << 16 (rows of 64 B)
   std::vector<uint32_t> h(257 * 16);
   uint32_t s = 12345;
-  for (auto &w : h) { s = s * 1103515245u + 12345u; w = ((s >> 8) % 257) * 64u << 16; }
-  uint32_t *g, *out;
-  hipMalloc(&g, h.size() * 4); hipMemcpy(g, h.data(), h.size() * 4, hipMemcpyHostToDevice);
-  int ncu = 256; hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-  hipMalloc(&out, (size_t)ncu * 16 * 256 * 4);
-  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
-  const int steps = 4096;
-  for (int bpc : {1, 2, 4, 8}) {
-    const size_t lds = 160 * 1024 / bpc - 1024;  // limits blocks per CU
-    for (int chains : {1, 2, 4}) {
-      auto k = chains == 1 ? chain<1> : chains == 2 ? chain<2> : chain<4>;
-      const int grid = ncu * bpc;
-      hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, g, out, 64, 0);
-      hipEventRecord(a);
-      hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, g, out, steps, 0);
-      hipEventRecord(b); hipEventSynchronize(b);
-      float ms; hipEventElapsedTime(&ms, a, b);
-      const double cyc = ms * 1e-3 * 2.4e9;
-      printf("blocks/CU %d (waves/SIMD %d) chains %d: %.1f cycles per step per wave, %.2f lookups/cycle/CU\n",
-             bpc, bpc, chains, cyc / steps, (double)grid * 256 * steps * chains / (cyc * ncu));
-    }
+  for (auto &w : h) {
+    s = s * 1103515245u + 12345u;
+    w = (((s >> 8) % 257) * 64u << 16) | ((s >> 3) & 0x1FFu);
   }
+  uint32_t *g, *out;
+  (void)hipMalloc(&g, h.size() * 4);
+  (void)hipMemcpy(g, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+  int ncu = 256;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+  (void)hipMalloc(&out, (size_t)ncu * 16 * 256 * 4);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  const int steps = 4096;
+  for (int store = 0; store < 2; ++store)
+    for (int bpc : {2, 4, 8}) {
+      const size_t lds = 160 * 1024 / bpc - 1024;  // limits blocks per CU
+      for (int chains : {1, 2, 4}) {
+        auto k = store ? (chains == 1 ? chain<1, true> : chains == 2 ? chain<2, true> : chain<4, true>)
+                       : (chains == 1 ? chain<1, false> : chains == 2 ? chain<2, false> : chain<4, false>);
+        const int grid = ncu * bpc;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, g, out, 64);
+        (void)hipEventRecord(a);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, g, out, steps);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        const double cyc = ms * 1e-3 * 2.4e9;
+        printf("store %d waves/SIMD %d chains %d: %6.1f cyc/step/wave  %.2f lookups/cyc/CU\n",
+               store, bpc, chains, cyc / steps,
+               (double)grid * 256 * steps * chains / (cyc * ncu));
+      }
+    }
   return 0;
 }

@@ -254,8 +254,8 @@ def test_full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
-def test_encode_unordered_spans_fallback(codec, corpus):
-    # non-monotone spans take the lane-per-string kernels; same bytes
+def test_encode_unordered_spans(codec, corpus):
+    # spans in any order: same bytes, dense output in span order
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
     rng = np.random.default_rng(5)
     idx = rng.permutation(len(ln))[:2000]
@@ -266,9 +266,8 @@ def test_encode_unordered_spans_fallback(codec, corpus):
         assert enc[o[j]:o[j] + l[j]].tobytes() == want
 
 
-def test_encode_gapped_spans_tiles(codec, corpus):
-    # monotone spans with gaps between strings (header-block framing bytes)
-    # stay on the tile engine
+def test_encode_gapped_spans(codec, corpus):
+    # spans with gaps between strings (header-block framing bytes)
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
     rng = np.random.default_rng(6)
     gaps = rng.integers(0, 9, len(ln))
@@ -284,3 +283,98 @@ def test_encode_gapped_spans_tiles(codec, corpus):
     total = int(corpus["enc_len"].astype(np.int64).sum())
     assert (l == corpus["enc_len"].astype(np.int64)).all()
     assert (enc[:total] == corpus["enc"]).all()
+
+
+def _mixed_strings(rng, big_len):
+    """Empty, short, long and one stage-sized string (codes > 24 KiB, so the
+    encoder's direct-to-HBM path runs); alphabet A and uniform bytes."""
+    a = np.frombuffer(synth.ALPHABET_A, dtype=np.uint8)
+    strs = []
+    for i in range(700):
+        k = int(rng.integers(0, 5))
+        n = [0, int(rng.integers(1, 16)), int(rng.integers(16, 300)),
+             int(rng.integers(300, 5000)), int(rng.integers(1, 64))][k]
+        if i % 3:
+            strs.append(bytes(rng.choice(a, n)))
+        else:
+            strs.append(bytes(rng.integers(0, 256, n).astype(np.uint8)))
+    strs[350] = bytes(rng.choice(a, big_len))
+    return strs
+
+
+def test_mixed_lengths_roundtrip(codec):
+    rng = np.random.default_rng(21)
+    strs = _mixed_strings(rng, 40000)
+    ln = np.array([len(x) for x in strs], dtype=np.int64)
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]])
+    plain = np.frombuffer(b"".join(strs), dtype=np.uint8)
+    enc, o, l, s = encode_dev(codec, plain, off, ln)
+    assert (s == 0).all()
+    want = [oracle.encode(x) for x in strs]
+    assert (l == np.array([len(w) for w in want])).all()
+    assert (o == np.concatenate([[0], np.cumsum(l)[:-1]])).all()  # dense
+    for j in range(len(strs)):
+        assert enc[o[j]:o[j] + l[j]].tobytes() == want[j], j
+    dst, do, dl, ds = decode_dev(codec, enc, o, l)
+    assert (ds == 0).all() and (dl == ln).all()
+    assert_disjoint(do, dl, int(q.decode_slot_size(l).sum()))
+    for j in range(len(strs)):
+        assert dst[do[j]:do[j] + dl[j]].tobytes() == strs[j], j
+
+
+def test_encode_dst_cap_too_small(codec, corpus):
+    # strings whose encoding would pass dst_cap get NOMEM; nothing is written
+    # at or past dst_cap; the others are exact
+    torch = torch_mod()
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    n = 3000
+    want_len = corpus["enc_len"][:n].astype(np.int64)
+    cap = int(want_len.sum()) // 2
+    src = to_dev(plain)
+    dst = torch.full((cap + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans_dev(off[:n], ln[:n]), dst[:cap], out)
+    o, l, s = q.unpack_out(out)
+    d = dst.cpu().numpy()
+    assert (d[cap:] == 0xA5).all()
+    assert set(np.unique(s)) <= {0, q.QH_ERR_NOMEM}
+    ok = s == 0
+    assert ok.any() and (~ok).any()
+    assert (o[ok] + l[ok] <= cap).all()
+    for j in np.nonzero(ok)[0]:
+        want = oracle.encode(plain[off[j]:off[j] + ln[j]].tobytes())
+        assert d[o[j]:o[j] + l[j]].tobytes() == want
+
+
+@pytest.mark.parametrize("kind", ["fsm", "lut", "fsm2"])
+def test_decoder_variants(kind, corpus):
+    """Every decoder (the default 4-bit FSM, QHUFF_DECODER=lut -- the 12-bit
+    table -- and QHUFF_DECODER=fsm2 -- two strings per lane) gives the
+    oracle's bytes and statuses."""
+    import os
+    from nghttp3_amd import HuffmanBatchCodec
+    old = os.environ.get("QHUFF_DECODER")
+    os.environ["QHUFF_DECODER"] = kind
+    try:
+        c = HuffmanBatchCodec(device=0)
+    finally:
+        if old is None:
+            del os.environ["QHUFF_DECODER"]
+        else:
+            os.environ["QHUFF_DECODER"] = old
+    try:
+        bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+        dst, o, l, s = decode_dev(c, bad, boff, blen)
+        assert (s == corpus["bad_status"]).all()
+        bolen = corpus["bad_out_len"].astype(np.int64)
+        ooff = np.concatenate([[0], np.cumsum(bolen)])
+        for i in np.nonzero(s == 0)[0]:
+            assert dst[o[i]:o[i] + l[i]].tobytes() == corpus["bad_out"][ooff[i]:ooff[i + 1]].tobytes()
+        enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+        dst, o, l, s = decode_dev(c, enc, eoff, elen)
+        assert (s == 0).all()
+        plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+        for i in range(0, len(ln), 5):
+            assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes()
+    finally:
+        c.close()
