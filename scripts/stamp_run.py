@@ -17,11 +17,7 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
-    "enc_count": ({11: "setup", 12: "rounds", 13: "lens+scan"}, 14, 15, None),
-    "enc_emit": ({0: "setup", 1: "load+cb", 2: "carry_scan", 3: "emit", 4: "copy"}, 9, 10, None),
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
-    "dec_chunks": ({0: "window", 1: "map+load", 2: "pass1", 3: "fixup", 4: "scan+pass2",
-                    5: "copy", 6: "results"}, 9, 10, 8),
 }
 
 
@@ -52,8 +48,6 @@ def main():
     read()
     reps = 5
     runs = {
-        "enc_count": lambda: codec.encode_count_dev(src, spans, hlen),
-        "enc_emit": lambda: codec.encode_dev(src, spans, enc, eout),
         "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
     }
     only = os.environ.get("KERNELS")
