@@ -230,14 +230,21 @@ class HuffmanBatchCodec:
         return src, spans, nbytes
 
     # -- host batches (library stages H2D / D2H) ----------------------------
-    def decode_host(self, src, spans):
-        """Decode packed host strings; returns (dst uint8, out SPAN_OUT_DTYPE)."""
+    def decode_host(self, src, spans, dst=None, out=None):
+        """Decode packed host strings; returns (dst uint8, out SPAN_OUT_DTYPE).
+
+        `dst` / `out` may be caller-provided (e.g. numpy views of pinned
+        torch tensors: the copies are then direct DMA)."""
         src = np.ascontiguousarray(src, dtype=np.uint8)
         spans = np.ascontiguousarray(spans, dtype=SPAN_IN_DTYPE)
         n = spans.size
         cap = int(self._lib.qh_decode_dst_size(spans.ctypes.data_as(ctypes.c_void_p), n))
-        dst = np.zeros(max(cap, 1), dtype=np.uint8)
-        out = np.zeros(n, dtype=SPAN_OUT_DTYPE)
+        if dst is None:
+            dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        assert dst.dtype == np.uint8 and dst.flags.c_contiguous and dst.size >= cap
+        if out is None:
+            out = np.zeros(n, dtype=SPAN_OUT_DTYPE)
+        assert out.dtype == SPAN_OUT_DTYPE and out.size >= n
         _lib.check(self._lib.qh_decode_batch(self._ctx, src.ctypes.data_as(ctypes.c_void_p),
                                              spans.ctypes.data_as(ctypes.c_void_p), n,
                                              dst.ctypes.data_as(ctypes.c_void_p), cap,

@@ -18,6 +18,8 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
+    "enc_lens": ({11: "window", 12: "passes", 13: "results"}, 14, 15, None),
+    "enc_lanes": ({0: "window", 1: "codes", 2: "copy"}, 10, 10, None),
 }
 
 
@@ -49,6 +51,8 @@ def main():
     reps = 5
     runs = {
         "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
+        "enc_lens": lambda: codec.encode_count_dev(src, spans, hlen),
+        "enc_lanes": lambda: codec.encode_dev(src, spans, enc, eout),
     }
     only = os.environ.get("KERNELS")
     for kern, fn in runs.items():
