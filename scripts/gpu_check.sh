@@ -28,7 +28,7 @@ run() {  # run NAME LIMIT CMD...
 
 for s in $STEPS; do
   case $s in
-    test)  run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    test)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
     bench) run bench 600 python bench.py && grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
     prof)  ( cd /tmp && export TMPDIR=/tmp && run rocprof 600 rocprofv3 --kernel-trace --stats \
