@@ -346,26 +346,36 @@ def test_encode_dst_cap_too_small(codec, corpus):
         assert d[o[j]:o[j] + l[j]].tobytes() == want
 
 
-@pytest.mark.parametrize("kind", ["fsm", "lut", "fsm2"])
-def test_decoder_variants(kind, corpus):
-    """Every decoder (the default 4-bit FSM, QHUFF_DECODER=lut -- the 12-bit
-    table -- and QHUFF_DECODER=fsm2 -- two strings per lane) gives the
-    oracle's bytes and statuses."""
+DECODERS = ["fsm", "lut", "fsm2", "peek11", "peek10", "peek12", "peek11_8"]
+
+
+def codec_of(kind):
     import os
     from nghttp3_amd import HuffmanBatchCodec
     old = os.environ.get("QHUFF_DECODER")
     os.environ["QHUFF_DECODER"] = kind
     try:
-        c = HuffmanBatchCodec(device=0)
+        return HuffmanBatchCodec(device=0)
     finally:
         if old is None:
             del os.environ["QHUFF_DECODER"]
         else:
             os.environ["QHUFF_DECODER"] = old
+
+
+@pytest.mark.parametrize("kind", DECODERS)
+def test_decoder_variants(kind, corpus, errors, kat, codec):
+    """Every decoder (the 4-bit FSM, QHUFF_DECODER=lut -- the 12-bit table,
+    fsm2 -- two strings per lane, peekW -- W-bit peek table in lock-step)
+    gives the oracle's bytes and statuses: golden corpus, corrupted strings,
+    the reference's error verdicts, RFC vectors, and mixed lengths 0-5000 B
+    over alphabet A and all 256 byte values (long codes, EOS-prefix ends)."""
+    c = codec_of(kind)
     try:
         bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
         dst, o, l, s = decode_dev(c, bad, boff, blen)
         assert (s == corpus["bad_status"]).all()
+        assert (l == corpus["bad_out_len"].astype(np.int64)).all()
         bolen = corpus["bad_out_len"].astype(np.int64)
         ooff = np.concatenate([[0], np.cumsum(bolen)])
         for i in np.nonzero(s == 0)[0]:
@@ -373,8 +383,40 @@ def test_decoder_variants(kind, corpus):
         enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
         dst, o, l, s = decode_dev(c, enc, eoff, elen)
         assert (s == 0).all()
+        assert_disjoint(o, l, int(q.decode_slot_size(elen.astype(np.int64)).sum()))
         plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
-        for i in range(0, len(ln), 5):
+        for i in range(len(ln)):
             assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes()
+        strs = [bytes.fromhex(x["hex"]) for x in errors["whole"]]
+        src, sp = q.pack_strings(strs)
+        dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+        for i, x in enumerate(errors["whole"]):
+            assert s[i] == x["status"], x
+            if x["status"] == 0:
+                assert dst[o[i]:o[i] + l[i]].tobytes().hex() == x["out_hex"]
+        src, sp = q.pack_strings([bytes.fromhex(v["huffman_hex"]) for v in kat])
+        dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+        for i, v in enumerate(kat):
+            assert s[i] == 0 and dst[o[i]:o[i] + l[i]].tobytes() == v["plain"].encode()
+        rng = np.random.default_rng(77)
+        strs = _mixed_strings(rng, 9000)
+        encs = [oracle.encode(x) for x in strs]
+        src, sp = q.pack_strings(encs)
+        dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+        assert (s == 0).all()
+        for j in range(len(strs)):
+            assert dst[o[j]:o[j] + l[j]].tobytes() == strs[j], j
+        # random bytes as Huffman input: statuses and outputs as the oracle
+        rb = [bytes(rng.integers(0, 256, int(rng.integers(0, 200))).astype(np.uint8))
+              for _ in range(3000)]
+        rb += [e[:-1] for e in encs[:300] if len(e) > 1]  # truncated strings
+        src, sp = q.pack_strings(rb)
+        want_dst, want_slot, want_len, want_st = oracle.decode_batch(src, sp["off"], sp["len"])
+        dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+        assert (s == want_st.astype(np.int64)).all()
+        assert (l == want_len.astype(np.int64)).all()
+        for j in np.nonzero(s == 0)[0]:
+            ws = int(want_slot[j])
+            assert dst[o[j]:o[j] + l[j]].tobytes() == want_dst[ws:ws + int(want_len[j])].tobytes()
     finally:
         c.close()
