@@ -163,10 +163,11 @@ QH_EXPORT int qh_ctx_last_stats(qh_ctx *ctx, qh_batch_stats *stats);
 /* Destination sizing.  A decoded string never exceeds the reference's
  * estimate_decode_length(len) = len * 8 / 5 (huffman.h:113-115; the caller
  * of the reference sizes its rcbuf from it, qpack.c:2977,3065,3591,3677).
- * Batch decode gives string i a slot of len_i * 8 / 5 + 16 bytes, slots in
- * string order and back to back, so qh_decode_dst_size(in, n) = sum of
- * (len * 8 / 5 + 16) is what a batch needs; out[i].off is the start of the
- * slot and out[i].len the decoded length.  The other bytes of a slot are
+ * Batch decode gives string i a slot of round_up(len_i * 8 / 5 + 16, 64)
+ * bytes, slots in string order and back to back (so every slot starts
+ * 64-byte aligned relative to dst), so qh_decode_dst_size(in, n) = the sum
+ * of the slots is what a batch needs; out[i].off is the start of the slot
+ * and out[i].len the decoded length.  The other bytes of a slot are
  * unspecified.  A string whose slot does not fit in dst_cap gets
  * QH_ERR_NOMEM; nothing is written at or past dst_cap.
  * Encode output is dense: out[i].off = sum_{j<i} encode_count(string j);

@@ -153,9 +153,10 @@ constexpr uint64_t kStMask = (1ull << 62) - 1;
 
 // Output slot of a string of `len` encoded bytes in a batch decode
 // (include/qhuff.h): the reference's estimate_decode_length
-// (huffman.h:113-115) + 16 spare bytes.
+// (huffman.h:113-115) + 16 spare bytes, rounded up to 64 bytes so that every
+// slot starts 64-byte aligned (decoders write whole 64-byte sectors).
 __host__ __device__ __forceinline__ uint64_t qh_dec_slot(uint32_t len) {
-  return (uint64_t)len * 8 / 5 + 16;
+  return ((uint64_t)len * 8 / 5 + 16 + 63) & ~(uint64_t)63;
 }
 
 // LDS image of the decode FSM (qh_lane_dec.inc): rows padded to 17 dwords so

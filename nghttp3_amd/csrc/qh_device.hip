@@ -41,6 +41,7 @@
 #include "qh_lane_dec2.inc"  // decoder: 4-bit FSM, two strings per lane
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #include "qh_peek_dec.inc"   // decoder: W-bit peek table, lock-step lanes
+#include "qh_dec3.inc"       // decoder (default): plan + task-queue lanes
 #include "qh_lane_enc.inc"   // encoder: lengths (chunks), codes (lanes)
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)

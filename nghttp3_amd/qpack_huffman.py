@@ -58,9 +58,9 @@ def huffman_estimate_decode_length(n: int) -> int:
 
 def decode_slot_size(n):
     """Bytes a string of n encoded bytes owns in the batch decode output:
-    estimate_decode_length + 16 (include/qhuff.h).  Works on ints and on
-    numpy / torch integer arrays."""
-    return n * 8 // 5 + 16
+    estimate_decode_length + 16, rounded up to 64 (include/qhuff.h).  Works
+    on ints and on numpy / torch integer arrays."""
+    return (n * 8 // 5 + 16 + 63) // 64 * 64
 
 
 def huffman_encode_count(src) -> int:

@@ -346,7 +346,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
         assert d[o[j]:o[j] + l[j]].tobytes() == want
 
 
-DECODERS = ["fsm", "lut", "fsm2", "peek11", "peek10", "peek12", "peek11_8"]
+DECODERS = ["run", "fsm", "lut", "fsm2", "peek11", "peek10", "peek12", "peek11_8"]
 
 
 def codec_of(kind):
