@@ -1,2 +1,2 @@
-for d in 0 0 1 3; do QHUFF_DEBUG=$d QHUFF_DECODER=run timeout -k 10 120 python -u scripts/dec_variants.py --kinds run --reps 5 2>&1 | grep -E "^\{" | sed "s/^/dbg=$d /" | cut -c1-160; done
-for b in 1 2; do QHUFF_BPC=$b QHUFF_DEBUG=3 QHUFF_DECODER=run timeout -k 10 120 python -u scripts/dec_variants.py --kinds run --reps 5 2>&1 | grep -E "^\{" | sed "s/^/dbg=3 bpc=$b /" | cut -c1-160; done
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-host-path > gpurun_out/b1.log 2>&1 || exit $?
+grep '^{' gpurun_out/b1.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', d['value'], 'dec', d['extra']['decode_GiBps'], 'enc', d['extra']['encode_GiBps']); [print(k, v['avg_us']) for k, v in d['extra']['kernels'].items()]"

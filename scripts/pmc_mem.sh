@@ -1,0 +1,20 @@
+#!/bin/bash
+# Memory-path counters (L1/TLB/L2) for bench.py --profile-only.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1
+OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for group in \
+  "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum" \
+  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_THRASHING_STALL_sum" \
+  "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_BUSY_avr TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum" \
+  "TCP_TCC_WRITE_REQ_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCP_LATENCY_sum" ; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $group --output-format csv -d "$OUT/g$i" -o run -- \
+     python3 "$ROOT/bench.py" --steps 2 --warmup 1 --profile-only > "$OUT/g$i.log" 2>&1
+  rc=$?; echo "group $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/g$i.log"; exit $rc; fi
+done
+python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E 'qhk' | sed 's/  /\n   /g'

@@ -18,7 +18,7 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
-    "enc_lens": ({11: "window", 12: "passes", 13: "results"}, 14, 15, None),
+    "enc_lens": ({0: "setup", 1: "loads", 2: "lookups", 3: "tail"}, 10, 10, None),
     "enc_lanes": ({0: "window", 1: "codes", 2: "copy"}, 10, 10, None),
 }
 
