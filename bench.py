@@ -163,7 +163,8 @@ def main():
         "qh_k_dec_peek": enc_bytes + total + 32 * n,
         "qh_k_dec_run": enc_bytes + total + 32 * n + 4 * n,  # + perm
         "qh_k_dec_plan": 16 * n + 8 * n + 4 * n,           # spans in, slots + perm out
-        "qh_k_enc_lens2": total + 16 * n + 8 * n,
+        "qh_k_enc_lens_stream": total + 16 * n + 8 * n,
+        "qh_k_enc_lens_lane": total + 16 * n + 8 * n,
         "qh_k_dec_reserve": 16 * n,                      # spans in
         "qh_k_enc_lens": total + 16 * n + 8 * n,         # D + spans in + len/status out
         "qh_k_enc_lanes": total + enc_bytes + 16 * n + 8 * n + 16 * n,  # D + E + spans

@@ -22,7 +22,39 @@ __device__ unsigned long long g_stamps[16];
   if (threadIdx.x == 0)                                                      \
     for (int _k = 0; _k < 16; ++_k)                                          \
       if (_st_a[_k]) atomicAdd(&g_stamps[_k], _st_a[_k]);
+// The same as an object a helper function can take by reference.
+struct StampAcc {
+  unsigned long long t, a[16], t0, r0;
+  __device__ void init() {
+    t = t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 16; ++k) a[k] = 0;
+  }
+  __device__ void st(int k) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    a[k] += n - t;
+    t = n;
+  }
+  __device__ void count(int k, unsigned long long v) { a[k] += v; }
+  __device__ void wait_mem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+  __device__ void flush() {  // slots 12, 13: block lifetime in realtime (100 MHz) / memtime
+    const unsigned long long life = __builtin_amdgcn_s_memrealtime() - r0;
+    a[12] += life;
+    a[13] += __builtin_amdgcn_s_memtime() - t0;
+    if (threadIdx.x == 0) atomicMax(&g_stamps[14], life);  // slot 14: the longest block
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 14; ++k)
+        if (a[k]) atomicAdd(&g_stamps[k], a[k]);
+  }
+};
 #else
+struct StampAcc {
+  __device__ void init() {}
+  __device__ void st(int) {}
+  __device__ void count(int, unsigned long long) {}
+  __device__ void wait_mem() {}
+  __device__ void flush() {}
+};
 #define QH_ST_INIT()
 #define QH_ST(k)
 #define QH_ST_COUNT(k, v)

@@ -18,8 +18,10 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
-    "enc_lens": ({0: "setup", 1: "loads", 2: "lookups", 3: "tail"}, 10, 10, None),
-    "enc_lanes": ({0: "window", 1: "codes", 2: "copy"}, 10, 10, None),
+    "enc_lens": ({0: "head", 2: "loads", 3: "lookups", 4: "bar1", 5: "scan", 6: "tail"},
+                 10, 10, 11),
+    "enc_lanes": ({9: "head", 2: "owners", 3: "loads+len", 4: "scan", 5: "zero+bar",
+                   6: "emit", 7: "copy"}, 10, 10, 11),
 }
 
 
@@ -71,6 +73,9 @@ def main():
             print(f"  {nm:11s} {st[k] / tiles:9.0f} cyc/tile {st[k] / rounds:8.0f} cyc/round"
                   f"  {100 * st[k] / max(tot, 1):5.1f}%")
         print(f"  wave0 cycles/launch {tot / reps:.3e}")
+        if st[12]:
+            print(f"  block lifetime: {st[12] / reps * 10 / 1000:.0f} us-blocks/launch (realtime), "
+                  f"memtime/realtime = {st[13] / st[12] * 100:.0f} MHz, longest block {st[14] / 100:.1f} us")
 
 
 if __name__ == "__main__":

@@ -285,6 +285,23 @@ def test_encode_gapped_spans(codec, corpus):
     assert (enc[:total] == corpus["enc"]).all()
 
 
+def test_encode_overlapping_spans(codec, corpus):
+    # heavily overlapping spans (each string starts 3 bytes after the last)
+    # and windows mixing near and far spans: lengths and codes per string
+    plain = corpus["plain"]
+    rng = np.random.default_rng(8)
+    n = 3000
+    off = np.arange(n, dtype=np.int64) * 3
+    ln = rng.integers(0, 400, n).astype(np.int64)
+    far = rng.random(n) < 0.02
+    off[far] = rng.integers(0, plain.size - 400, int(far.sum()))
+    enc, o, l, s = encode_dev(codec, plain, off, ln)
+    assert (s == 0).all()
+    for j in range(n):
+        want = oracle.encode(plain[off[j]:off[j] + ln[j]].tobytes())
+        assert enc[o[j]:o[j] + l[j]].tobytes() == want, j
+
+
 def _mixed_strings(rng, big_len):
     """Empty, short, long and one stage-sized string (codes > 24 KiB, so the
     encoder's direct-to-HBM path runs); alphabet A and uniform bytes."""
@@ -418,5 +435,52 @@ def test_decoder_variants(kind, corpus, errors, kat, codec):
         for j in np.nonzero(s == 0)[0]:
             ws = int(want_slot[j])
             assert dst[o[j]:o[j] + l[j]].tobytes() == want_dst[ws:ws + int(want_len[j])].tobytes()
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("mode", ["stream", "lane", "chunks", "lanecodes", "lane_lanecodes"])
+def test_encode_length_passes(mode, corpus, digests):
+    """The encoder's passes: streaming lengths and codes (default), every
+    window's lengths left to the lane-per-string pass (QHUFF_DEBUG=4), the
+    chunk-engine lengths (QHUFF_ENCODER=chunks), lane-per-string codes
+    (QHUFF_DEBUG=8) and both lane passes (12) -- corpus lengths/codes, counts,
+    overlapping and scattered spans, and the full-size c2_U digest."""
+    import os
+    from nghttp3_amd import HuffmanBatchCodec
+    env = {"stream": {}, "lane": {"QHUFF_DEBUG": "4"},
+           "chunks": {"QHUFF_ENCODER": "chunks"}, "lanecodes": {"QHUFF_DEBUG": "8"},
+           "lane_lanecodes": {"QHUFF_DEBUG": "12"}}[mode]
+    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG", "QHUFF_ENCODER")}
+    for k in old:
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    try:
+        c = HuffmanBatchCodec(device=0)
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+    try:
+        torch = torch_mod()
+        test_corpus_encode(c, corpus)
+        test_corpus_encode_count(c, corpus)
+        test_encode_overlapping_spans(c, corpus)
+        test_encode_unordered_spans(c, corpus)
+        test_encode_gapped_spans(c, corpus)
+        d = digests["c2_U"]
+        src, spans, total = c.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_U)
+        ln = spans[:, 1] & 0xFFFFFFFF
+        enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8,
+                          device="cuda")
+        eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+        for _ in range(2):  # the second call reuses the other window-list counter
+            c.encode_dev(src, spans, enc, eout)
+            st = c.stats()
+            assert st["n_errors"] == 0 and st["out_bytes"] == d["enc_bytes"]
+            elen = (eout[:, 1] & 0xFFFFFFFF).to(torch.int32)
+            assert sha(elen.cpu().numpy().astype(np.uint32)) == d["enc_len_sha256"]
+            assert sha(enc[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
     finally:
         c.close()
