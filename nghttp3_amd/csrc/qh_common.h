@@ -41,7 +41,13 @@ struct StampAcc {
     const unsigned long long life = __builtin_amdgcn_s_memrealtime() - r0;
     a[12] += life;
     a[13] += __builtin_amdgcn_s_memtime() - t0;
-    if (threadIdx.x == 0) atomicMax(&g_stamps[14], life);  // slot 14: the longest block
+    if (threadIdx.x == 0) {
+      atomicMax(&g_stamps[14], life);  // slot 14: the longest block
+      // slots 7, 8, 9: ~(earliest start), latest start, latest end (realtime)
+      atomicMax(&g_stamps[7], ~r0);
+      atomicMax(&g_stamps[8], r0);
+      atomicMax(&g_stamps[9], r0 + life);
+    }
     if (threadIdx.x == 0)
       for (int k = 0; k < 14; ++k)
         if (a[k]) atomicAdd(&g_stamps[k], a[k]);

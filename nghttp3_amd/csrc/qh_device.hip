@@ -42,7 +42,8 @@
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #include "qh_peek_dec.inc"   // decoder: W-bit peek table, lock-step lanes
 #include "qh_dec3.inc"       // decoder (default): plan + task-queue lanes
-#include "qh_lane_enc.inc"   // encoder: lengths (chunks), codes (lanes)
+#include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes, chunks), codes (lanes)
+#include "qh_enc_stream.inc" // encoder (default codes): streaming region rounds
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
 

@@ -18,10 +18,10 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
-    "enc_lens": ({0: "head", 2: "loads", 3: "lookups", 4: "bar1", 5: "scan", 6: "tail"},
+    "enc_lens": ({0: "head", 2: "dma wait", 3: "lookups", 4: "scan", 5: "ends", 6: "tail"},
                  10, 10, 11),
-    "enc_lanes": ({9: "head", 2: "owners", 3: "loads+len", 4: "scan", 5: "zero+bar",
-                   6: "emit", 7: "copy"}, 10, 10, 11),
+    "enc_lanes": ({0: "head", 1: "wait+zero", 2: "bits+scan", 3: "starts", 4: "emit",
+                   5: "copy"}, 10, 10, 11),
 }
 
 
@@ -50,7 +50,7 @@ def main():
     codec.decode_dev(enc, eout, dec, dout)
     codec.sync()
     read()
-    reps = 5
+    reps = int(os.environ.get("REPS", 5))
     runs = {
         "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
         "enc_lens": lambda: codec.encode_count_dev(src, spans, hlen),
@@ -73,6 +73,10 @@ def main():
             print(f"  {nm:11s} {st[k] / tiles:9.0f} cyc/tile {st[k] / rounds:8.0f} cyc/round"
                   f"  {100 * st[k] / max(tot, 1):5.1f}%")
         print(f"  wave0 cycles/launch {tot / reps:.3e}")
+        if st[8] and reps == 1:
+            t0 = (~st[7]) & ((1 << 64) - 1)
+            print(f"  starts: first..last {(st[8] - t0) / 100:.1f} us after the first; "
+                  f"last end {(st[9] - t0) / 100:.1f} us after the first start")
         if st[12]:
             print(f"  block lifetime: {st[12] / reps * 10 / 1000:.0f} us-blocks/launch (realtime), "
                   f"memtime/realtime = {st[13] / st[12] * 100:.0f} MHz, longest block {st[14] / 100:.1f} us")

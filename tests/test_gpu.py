@@ -439,19 +439,23 @@ def test_decoder_variants(kind, corpus, errors, kat, codec):
         c.close()
 
 
-@pytest.mark.parametrize("mode", ["stream", "lane", "chunks", "lanecodes", "lane_lanecodes"])
+@pytest.mark.parametrize("mode", ["default", "lane", "chunks", "streamcodes", "streamcodes_lane",
+                                  "streamcodes_listed"])
 def test_encode_length_passes(mode, corpus, digests):
-    """The encoder's passes: streaming lengths and codes (default), every
-    window's lengths left to the lane-per-string pass (QHUFF_DEBUG=4), the
-    chunk-engine lengths (QHUFF_ENCODER=chunks), lane-per-string codes
-    (QHUFF_DEBUG=8) and both lane passes (12) -- corpus lengths/codes, counts,
-    overlapping and scattered spans, and the full-size c2_U digest."""
+    """The encoder's passes: streaming lengths + lane-per-string codes
+    (default), every window's lengths left to the lane-per-string pass
+    (QHUFF_DEBUG=4), the chunk-engine lengths (QHUFF_ENCODER=chunks), the
+    streaming codes kernel (QHUFF_CODES=stream) alone, with lane lengths, and
+    with every window listed to the lane codes pass (QHUFF_DEBUG=8) --
+    corpus lengths/codes, counts, overlapping and scattered spans, and the
+    full-size c2_U digest."""
     import os
     from nghttp3_amd import HuffmanBatchCodec
-    env = {"stream": {}, "lane": {"QHUFF_DEBUG": "4"},
-           "chunks": {"QHUFF_ENCODER": "chunks"}, "lanecodes": {"QHUFF_DEBUG": "8"},
-           "lane_lanecodes": {"QHUFF_DEBUG": "12"}}[mode]
-    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG", "QHUFF_ENCODER")}
+    env = {"default": {}, "lane": {"QHUFF_DEBUG": "4"},
+           "chunks": {"QHUFF_ENCODER": "chunks"}, "streamcodes": {"QHUFF_CODES": "stream"},
+           "streamcodes_lane": {"QHUFF_CODES": "stream", "QHUFF_DEBUG": "4"},
+           "streamcodes_listed": {"QHUFF_CODES": "stream", "QHUFF_DEBUG": "8"}}[mode]
+    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG", "QHUFF_ENCODER", "QHUFF_CODES")}
     for k in old:
         os.environ.pop(k, None)
     os.environ.update(env)
