@@ -9,6 +9,8 @@ namespace qhk {
 // out of the product library.
 #ifdef QH_STAMPS
 __device__ unsigned long long g_stamps[16];
+// per block (blockIdx.x < 8192): start (realtime), lifetime, HW_ID register
+__device__ unsigned long long g_blk[8192][3];
 #define QH_ST_INIT()                                                         \
   unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_a[16] = {0};
 #define QH_ST(k)                                                             \
@@ -47,6 +49,11 @@ struct StampAcc {
       atomicMax(&g_stamps[7], ~r0);
       atomicMax(&g_stamps[8], r0);
       atomicMax(&g_stamps[9], r0 + life);
+      if (blockIdx.x < 8192) {
+        g_blk[blockIdx.x][0] = r0;
+        g_blk[blockIdx.x][1] = life;
+        g_blk[blockIdx.x][2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      }
     }
     if (threadIdx.x == 0)
       for (int k = 0; k < 14; ++k)
