@@ -488,3 +488,29 @@ def test_encode_length_passes(mode, corpus, digests):
             assert sha(enc[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("alphabet", ["A", "U"])
+def test_zipf_lengths_roundtrip(codec, alphabet):
+    """Config-5 shape at reduced size: Zipf(s = 1.2) lengths 1..4096 (long
+    strings span many decoder iterations and length-pass rounds), packed;
+    encode against the oracle's batch encoder, then decode back."""
+    rng = np.random.default_rng(55)
+    n = 12000
+    ranks = np.arange(1, 4097, dtype=np.float64)
+    p = ranks ** -1.2
+    p /= p.sum()
+    ln = rng.choice(np.arange(1, 4097), size=n, p=p).astype(np.int64)
+    a = np.frombuffer(synth.ALPHABET_A if alphabet == "A" else synth.ALPHABET_U, dtype=np.uint8)
+    plain = a[rng.integers(0, len(a), int(ln.sum()))]
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]])
+    want_enc, want_off, want_len = oracle.encode_batch(plain, off, ln)[:3]
+    enc, o, l, s = encode_dev(codec, plain, off, ln)
+    assert (s == 0).all()
+    assert (l == np.asarray(want_len, dtype=np.int64)).all()
+    total = int(l.sum())
+    assert (enc[:total] == np.asarray(want_enc)[:total]).all()
+    dst, do, dl, ds = decode_dev(codec, enc[:total], o, l)
+    assert (ds == 0).all() and (dl == ln).all()
+    for j in range(0, n, 37):
+        assert dst[do[j]:do[j] + dl[j]].tobytes() == plain[off[j]:off[j] + ln[j]].tobytes(), j
