@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the alphabet-U and Zipf-length measurements in extra.configs")
     ap.add_argument("--profile-only", action="store_true",
                     help="just run warmup+steps (for rocprofv3), minimal reporting")
     return ap.parse_args()
@@ -194,6 +196,55 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "algo_bytes_per_launch": kern[dom]["algo_bytes"]}
 
+    # ---- other BASELINE shapes on this GPU (reported in extra, never the value) ----
+    def measure(c_src, c_spans, c_total, reps=5):
+        c_n = c_spans.shape[0]
+        c_ln = c_spans[:, 1] & 0xFFFFFFFF
+        c_enc = torch.empty(int(((c_ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device=dev)
+        c_eout = torch.empty((c_n, 2), dtype=torch.int64, device=dev)
+        codec.encode_dev(c_src, c_spans, c_enc, c_eout)
+        torch.cuda.synchronize()
+        c_cap = int(q.decode_slot_size(c_eout[:, 1] & 0xFFFFFFFF).sum().item())
+        c_dec = torch.empty(max(c_cap, 1), dtype=torch.uint8, device=dev)
+        c_dout = torch.empty((c_n, 2), dtype=torch.int64, device=dev)
+        codec.decode_dev(c_enc, c_eout, c_dec, c_dout)
+        te = timed(lambda: codec.encode_dev(c_src, c_spans, c_enc, c_eout), reps)
+        td = timed(lambda: codec.decode_dev(c_enc, c_eout, c_dec, c_dout), reps)
+        c_ok = bool(((c_dout[:, 1] >> 32) == 0).all()) and bool(((c_dout[:, 1] & 0xFFFFFFFF) == c_ln).all())
+        if c_ok:
+            rep_d = torch.repeat_interleave(c_dout[:, 0], c_ln)
+            rep_p = torch.repeat_interleave(c_spans[:, 0], c_ln)
+            pos = torch.arange(c_total, device=dev, dtype=torch.int64) - rep_p
+            c_ok = bool((c_dec[rep_d + pos] == c_src[rep_p + pos]).all())
+            del rep_d, rep_p, pos
+        r = {"strings": c_n, "plain_bytes": c_total, "encode_GiBps": round(c_total / te / GIB, 2),
+             "decode_GiBps": round(c_total / td / GIB, 2),
+             "round_trip_GiBps": round(c_total / (te + td) / GIB, 2), "bit_exact": c_ok}
+        del c_enc, c_eout, c_dec, c_dout
+        return r
+
+    configs = None
+    if rank == 0 and world == 1 and not args.no_configs:
+        configs = {}
+        u_src, u_spans, u_total = codec.synth(args.seed, n, args.lo, args.hi, synth.ALPHABET_U)
+        configs["config3_alphabet_U"] = measure(u_src, u_spans, u_total)
+        del u_src, u_spans
+        # config 5 shape on one GPU: Zipf(s = 1.2) lengths 1..4096 over a synthetic
+        # alphabet-A text (seeded numpy draw of the lengths, device-generated bytes)
+        zr = np.random.default_rng(0x5EED0005)
+        ranks = np.arange(1, 4097, dtype=np.float64)
+        pz = ranks ** -1.2
+        pz /= pz.sum()
+        z_ln = zr.choice(np.arange(1, 4097), size=n, p=pz).astype(np.int64)
+        z_total = int(z_ln.sum())
+        z_src, _, z_have = codec.synth(args.seed + 5, max(1, z_total // 300 + 1), 300, 300,
+                                       synth.ALPHABET_A)
+        z_off = np.concatenate([[0], np.cumsum(z_ln)[:-1]])
+        z_sp = torch.from_numpy(np.stack([z_off, z_ln], axis=1)).to(dev)
+        configs["config5_zipf_1gpu"] = dict(measure(z_src, z_sp, z_total),
+                                            lengths="Zipf s=1.2 over 1..4096, mean %.0f B" % z_ln.mean())
+        del z_src, z_sp
+
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None
     if rank == 0 and world == 1 and not args.no_host_path:
@@ -266,7 +317,7 @@ def main():
             "cpu_baseline": cpu,
             "extra": {"decode_GiBps": round(total / t_dec / GIB, 2),
                       "encode_GiBps": round(total / t_enc / GIB, 2),
-                      "kernels": kern, "host_path": host_path},
+                      "kernels": kern, "host_path": host_path, "configs": configs},
         }
         print(json.dumps(line))
 

@@ -5,7 +5,8 @@ The HIP kernel looks the top W bits of a lane's 64-bit bit buffer up in a
 word per group of 4 lookups when <= 32 bits are buffered, feeds 1-bits past
 the end of the string, and sends escapes (codes > W bits, too few buffered
 bits, the end of the string) to a careful path: refill, then the
-end-of-string decision or one canonical symbol.  `peek_decode` is that
+end-of-string decision or canonical symbols (the first always, then while the
+next code is not a short one, up to 16).  `peek_decode` is that
 algorithm step for step; the tests compare it with the oracle (the
 reference's nibble FSM, lib/nghttp3_qpack_huffman.c:87-129) on the golden
 corpus, the corrupted strings, the error fixtures and random bytes, for every
@@ -69,18 +70,28 @@ def peek_decode(data, w, tab):
                 st["nb"] -= n
                 out.append(e >> 8)
                 continue
-            refill()  # careful path
-            sleft = total - (st["refills"] * 32 - st["nb"])
-            if sleft <= 0:
-                return (0, bytes(out)) if sleft == 0 else (-108, b"")
-            if sleft <= 7 and (st["bb"] >> (64 - sleft)) == (1 << sleft) - 1:
-                return 0, bytes(out)
-            sym, n = _canonical(st["bb"] >> 32)
-            if n > sleft or sym == G.EOS:
-                return -108, b""
-            st["bb"] = (st["bb"] << n) & MASK64
-            st["nb"] -= n
-            out.append(sym)
+            kc = 0  # careful path: canonical symbols while long codes follow
+            while True:
+                refill()
+                sleft = total - (st["refills"] * 32 - st["nb"])
+                if sleft <= 0:
+                    return (0, bytes(out)) if sleft == 0 else (-108, b"")
+                if sleft <= 7 and (st["bb"] >> (64 - sleft)) == (1 << sleft) - 1:
+                    return 0, bytes(out)
+                if kc:
+                    e2 = tab[st["bb"] >> (64 - w)]
+                    if e2 != ESC and st["nb"] - (e2 & 0xFF) >= 0:
+                        break
+                sym, n = _canonical(st["bb"] >> 32)
+                if n > sleft or sym == G.EOS:
+                    return -108, b""
+                st["bb"] = (st["bb"] << n) & MASK64
+                st["nb"] -= n
+                out.append(sym)
+                kc += 1
+                if kc == 16:
+                    break
+            break
 
 
 @pytest.fixture(scope="module", params=[10, 11, 12])
