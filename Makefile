@@ -6,13 +6,14 @@ ARCH    ?= gfx950
 CSRC    := nghttp3_amd/csrc
 LIBDIR  := nghttp3_amd/lib
 LIB     := $(LIBDIR)/libqhuff.so
+ARCHIVE := $(LIBDIR)/libqhuff.a
 ORACLE  := oracle/libqh_oracle.so
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 CFLAGS   := -std=c11 -O2 -fPIC -fvisibility=hidden -Wall -Wextra
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ARCHIVE) $(ORACLE)
 
 $(CSRC)/qh_tables.h: nghttp3_amd/tools/gen_tables.py
 	python3 nghttp3_amd/tools/gen_tables.py $@
@@ -28,6 +29,12 @@ $(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $
 $(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
+# Static archive of the same two objects, for linking into libnghttp3 in
+# place of the reference's Huffman objects.
+$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
+	rm -f $@
+	ar rcs $@ $^
+
 # Phase-timer build for kernel development (not loaded unless QHUFF_LIB
 # points at it).
 STAMPS := $(LIBDIR)/libqhuff_stamps.so
@@ -42,6 +49,6 @@ $(ORACLE): oracle/qh_oracle.c oracle/qh_oracle.h
 	$(CC) -std=c11 -O2 -mavx2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIB) $(STAMPS) $(ORACLE)
+	rm -f $(LIBDIR)/*.o $(LIB) $(ARCHIVE) $(STAMPS) $(ORACLE)
 
 .PHONY: all clean stamps
