@@ -18,6 +18,7 @@ from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
+    "dec_peek": ({0: "window", 4: "start", 3: "top wait", 2: "body", 1: "end"}, 11, 10, None),
     "enc_lens": ({0: "head", 2: "dma wait", 3: "lookups", 4: "scan", 5: "ends", 6: "tail"},
                  10, 10, 11),
     "enc_lanes": ({0: "head", 1: "wait+zero", 2: "bits+scan", 3: "starts", 4: "emit",
@@ -53,6 +54,7 @@ def main():
     reps = int(os.environ.get("REPS", 5))
     runs = {
         "dec_lanes": lambda: codec.decode_dev(enc, eout, dec, dout),
+        "dec_peek": lambda: codec.decode_dev(enc, eout, dec, dout),
         "enc_lens": lambda: codec.encode_count_dev(src, spans, hlen),
         "enc_lanes": lambda: codec.encode_dev(src, spans, enc, eout),
     }
