@@ -364,7 +364,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
 
 
 DECODERS = ["run", "fsm", "lut", "fsm2", "peek11ld", "peek11", "peek11d", "peek10", "peek12",
-            "peek11_8", "peek11_2", "peek11_2w5", "snake11d"]
+            "peek11_8", "peek11_2", "peek11_2w5", "snake11d", "peek10ld"]
 
 
 def codec_of(kind):
