@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--hi", type=int, default=256)
     ap.add_argument("--alphabet", default="A")
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--kinds", default="peek11ld,peek11,peek11d")
+    ap.add_argument("--kinds", default="peek11lda,peek11ld,peek11")
     args = ap.parse_args()
     import torch
     from nghttp3_amd import HuffmanBatchCodec, synth

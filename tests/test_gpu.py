@@ -363,7 +363,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
         assert d[o[j]:o[j] + l[j]].tobytes() == want
 
 
-DECODERS = ["run", "fsm", "lut", "fsm2", "peek11ld", "peek11", "peek11d", "peek10", "peek12",
+DECODERS = ["run", "fsm", "lut", "fsm2", "peek11ld", "peek11lda", "peek11", "peek11d", "peek10", "peek12",
             "peek11_8", "peek11_2", "peek11_2w5", "snake11d", "peek10ld"]
 
 
