@@ -26,12 +26,16 @@ $(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
+$(LIBDIR)/qh_qpack.o: $(CSRC)/qh_qpack.c include/qhuff.h
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 # Static archive of the same two objects, for linking into libnghttp3 in
 # place of the reference's Huffman objects.
-$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o
+$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o
 	rm -f $@
 	ar rcs $@ $^
 

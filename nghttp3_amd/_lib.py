@@ -88,6 +88,17 @@ EXPORTED_FUNCTIONS = (
     "qh_decode_batch",
     "qh_encode_count_batch",
     "qh_encode_batch",
+    # QPACK field-line framing (csrc/qh_qpack.c, bound in qpack.py)
+    "qh_qpack_scan_field_section",
+    "qh_qpack_scan_blocks",
+    "qh_qpack_scan_encoder_stream",
+    "qh_qpack_put_varint_len",
+    "qh_qpack_put_varint",
+    "qh_qpack_write_indexed",
+    "qh_qpack_write_indexed_name",
+    "qh_qpack_write_literal",
+    "qh_qpack_literal_bound",
+    "qh_qpack_write_sections",
     "qh_ctx_enable_timing",
     "qh_ctx_kernel_times",
     "qh_synth_spans",

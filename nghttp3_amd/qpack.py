@@ -1,0 +1,262 @@
+"""QPACK field-line framing around the batch Huffman engine (SURVEY.md
+section 8(f) rows 1-2), over the C-ABI of nghttp3_amd/csrc/qh_qpack.c.
+
+* ``scan_field_section`` / ``scan_blocks`` / ``scan_encoder_stream`` --
+  the framing of nghttp3_qpack_decoder_read_request
+  (lib/nghttp3_qpack.c:3347-3800) and nghttp3_qpack_decoder_read_encoder
+  (:2815-3150), returning field lines and (off, len, flags) string spans.
+* ``write_indexed`` / ``write_indexed_name`` / ``write_literal`` -- the
+  representation writers (qpack.c:1851-2069) with the reference's
+  Huffman-iff-shorter choice.
+* ``FieldSectionDecoder`` -- whole header blocks in, decoded strings out:
+  host-side scan, then every Huffman string of the batch in one
+  ``qh_decode_batch`` call on the GPU.
+
+Error values are the reference's: -401 DECOMPRESSION_FAILED, -402
+ENCODER_STREAM_ERROR, -109 HEADER_TOO_LARGE (nghttp3.h:224-259).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .qpack_huffman import SPAN_IN_DTYPE, SPAN_OUT_DTYPE, HuffmanBatchCodec
+
+QH_ERR_QPACK_HEADER_TOO_LARGE = -109
+QH_ERR_QPACK_DECOMPRESSION_FAILED = -401
+QH_ERR_QPACK_ENCODER_STREAM_ERROR = -402
+
+SPAN_HUFFMAN, SPAN_NAME = 0x1, 0x2
+(FL_INDEXED, FL_INDEXED_PB, FL_INDEXED_NAME, FL_INDEXED_NAME_PB, FL_LITERAL,
+ ES_INSERT_INDEXED, ES_INSERT, ES_SET_DTABLE_CAP, ES_DUPLICATE) = range(1, 10)
+FL_DYNAMIC, FL_NEVER = 0x1, 0x2
+
+FIELD_LINE_DTYPE = np.dtype([("index", "<u8"), ("opcode", "u1"), ("flags", "u1"),
+                             ("reserved", "<u2"), ("name", "<i4"), ("value", "<i4"),
+                             ("reserved2", "<u4")])
+assert FIELD_LINE_DTYPE.itemsize == 24
+
+
+class qh_section_prefix(ctypes.Structure):
+    _fields_ = [("ricnt", ctypes.c_uint64), ("delta_base", ctypes.c_uint64),
+                ("sign", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+_L = None
+
+
+def _load():
+    global _L
+    if _L is None:
+        lib = _lib.load()
+        c = ctypes
+        vp, sz, u64, u8, i32 = c.c_void_p, c.c_size_t, c.c_uint64, c.c_uint8, c.c_int
+        lib.qh_qpack_scan_field_section.argtypes = [vp, sz, u64, c.POINTER(qh_section_prefix), vp, sz,
+                                                    c.POINTER(sz), vp, sz, c.POINTER(sz)]
+        lib.qh_qpack_scan_field_section.restype = i32
+        lib.qh_qpack_scan_blocks.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, vp, vp]
+        lib.qh_qpack_scan_blocks.restype = i32
+        lib.qh_qpack_scan_encoder_stream.argtypes = [vp, sz, u64, vp, sz, c.POINTER(sz), vp, sz,
+                                                     c.POINTER(sz)]
+        lib.qh_qpack_scan_encoder_stream.restype = c.c_ssize_t
+        lib.qh_qpack_put_varint_len.argtypes = [u64, sz]
+        lib.qh_qpack_put_varint_len.restype = sz
+        lib.qh_qpack_put_varint.argtypes = [vp, u64, sz]
+        lib.qh_qpack_put_varint.restype = vp
+        lib.qh_qpack_write_indexed.argtypes = [vp, u8, u64, sz]
+        lib.qh_qpack_write_indexed.restype = sz
+        lib.qh_qpack_write_indexed_name.argtypes = [vp, u8, u64, sz, vp, sz]
+        lib.qh_qpack_write_indexed_name.restype = sz
+        lib.qh_qpack_write_literal.argtypes = [vp, u8, sz, vp, sz, vp, sz]
+        lib.qh_qpack_write_literal.restype = sz
+        lib.qh_qpack_literal_bound.argtypes = [sz, sz]
+        lib.qh_qpack_literal_bound.restype = sz
+        lib.qh_qpack_write_sections.argtypes = [vp, vp, vp, vp, sz, vp, vp, sz, vp]
+        lib.qh_qpack_write_sections.restype = i32
+        _L = lib
+    return _L
+
+
+def _u8(data):
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) \
+        else np.ascontiguousarray(data, dtype=np.uint8)
+    if a.size == 0:
+        a = np.zeros(1, dtype=np.uint8)[:0]
+    return a
+
+
+def _vp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def scan_field_section(buf, base_off: int = 0):
+    """One complete field section -> (status, (ricnt, sign, delta_base) or
+    None, lines FIELD_LINE_DTYPE, spans SPAN_IN_DTYPE)."""
+    lib = _load()
+    src = _u8(buf)
+    cap = src.size + 1  # every line and string takes at least one byte
+    lines = np.zeros(cap, dtype=FIELD_LINE_DTYPE)
+    spans = np.zeros(cap, dtype=SPAN_IN_DTYPE)
+    pf = qh_section_prefix()
+    nl, ns = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    rv = lib.qh_qpack_scan_field_section(_vp(src), src.size, base_off, ctypes.byref(pf), _vp(lines),
+                                         cap, ctypes.byref(nl), _vp(spans), cap, ctypes.byref(ns))
+    if rv != 0:
+        return rv, None, lines[:0], spans[:0]
+    return 0, (pf.ricnt, pf.sign, pf.delta_base), lines[:nl.value], spans[:ns.value]
+
+
+def scan_blocks(src, blocks):
+    """Batch of field sections (blocks: SPAN_IN_DTYPE into src) ->
+    (lines, spans, line_start, span_start, status)."""
+    lib = _load()
+    src = _u8(src)
+    blocks = np.ascontiguousarray(blocks, dtype=SPAN_IN_DTYPE)
+    nb = blocks.size
+    cap = int(blocks["len"].sum(dtype=np.uint64)) + 1
+    lines = np.zeros(cap, dtype=FIELD_LINE_DTYPE)
+    spans = np.zeros(cap, dtype=SPAN_IN_DTYPE)
+    ls = np.zeros(nb + 1, dtype=np.uint32)
+    ss = np.zeros(nb + 1, dtype=np.uint32)
+    st = np.zeros(max(nb, 1), dtype=np.int32)
+    _lib.check(lib.qh_qpack_scan_blocks(_vp(src), _vp(blocks), nb, _vp(lines), cap, _vp(spans), cap,
+                                        _vp(ls), _vp(ss), _vp(st)), "qh_qpack_scan_blocks")
+    return lines[:ls[nb]], spans[:ss[nb]], ls, ss, st[:nb]
+
+
+def scan_encoder_stream(buf, base_off: int = 0):
+    """-> (consumed bytes or negative error, instructions, spans)."""
+    lib = _load()
+    src = _u8(buf)
+    cap = src.size + 1
+    lines = np.zeros(cap, dtype=FIELD_LINE_DTYPE)
+    spans = np.zeros(cap, dtype=SPAN_IN_DTYPE)
+    nl, ns = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    rv = lib.qh_qpack_scan_encoder_stream(_vp(src), src.size, base_off, _vp(lines), cap,
+                                          ctypes.byref(nl), _vp(spans), cap, ctypes.byref(ns))
+    return rv, lines[:nl.value], spans[:ns.value]
+
+
+def put_varint(n: int, prefix: int, fb: int = 0) -> bytes:
+    lib = _load()
+    buf = (ctypes.c_uint8 * 16)(fb)
+    end = lib.qh_qpack_put_varint(buf, n, prefix)
+    k = end - ctypes.addressof(buf)
+    assert k == lib.qh_qpack_put_varint_len(n, prefix)
+    return bytes(buf[:k])
+
+
+def _write(fn, *args, bound):
+    buf = np.zeros(bound, dtype=np.uint8)
+    n = fn(_vp(buf), *args)
+    return buf[:n].tobytes()
+
+
+def write_indexed(fb: int, idx: int, prefix: int) -> bytes:
+    return _write(_load().qh_qpack_write_indexed, fb, idx, prefix, bound=16)
+
+
+def write_indexed_name(fb: int, nameidx: int, prefix: int, value: bytes) -> bytes:
+    """qpack_encoder_write_indexed_name (qpack.c:1851-1896)."""
+    lib = _load()
+    v = _u8(value)
+    return _write(lib.qh_qpack_write_indexed_name, fb, nameidx, prefix, _vp(v), v.size,
+                  bound=lib.qh_qpack_literal_bound(0, v.size))
+
+
+def write_literal(fb: int, prefix: int, name: bytes, value: bytes) -> bytes:
+    """qpack_encoder_write_literal (qpack.c:1944-2006)."""
+    lib = _load()
+    nm, v = _u8(name), _u8(value)
+    return _write(lib.qh_qpack_write_literal, fb, prefix, _vp(nm), nm.size, _vp(v), v.size,
+                  bound=lib.qh_qpack_literal_bound(nm.size, v.size))
+
+
+def write_sections(plain, strs, lines, line_start):
+    """Batch writer (qh_qpack_write_sections): -> (dst uint8, sections
+    SPAN_IN_DTYPE), every section with a zero prefix."""
+    lib = _load()
+    plain = _u8(plain)
+    strs = np.ascontiguousarray(strs, dtype=SPAN_IN_DTYPE)
+    lines = np.ascontiguousarray(lines, dtype=FIELD_LINE_DTYPE)
+    line_start = np.ascontiguousarray(line_start, dtype=np.uint32)
+    nsec = line_start.size - 1
+    cap = int(strs["len"].sum(dtype=np.uint64)) + 20 * lines.size + 20 * nsec + 1
+    dst = np.zeros(cap, dtype=np.uint8)
+    sections = np.zeros(max(nsec, 1), dtype=SPAN_IN_DTYPE)
+    _lib.check(lib.qh_qpack_write_sections(_vp(plain), _vp(strs), _vp(lines), _vp(line_start), nsec,
+                                           None, _vp(dst), cap, _vp(sections)),
+               "qh_qpack_write_sections")
+    end = int(sections["off"][nsec - 1] + sections["len"][nsec - 1]) if nsec else 0
+    return dst[:end], sections[:nsec]
+
+
+def synth_field_sections(seed: int, nblocks: int, fields=(4, 20), namelen=(4, 24),
+                         valuelen=(1, 128), alphabet: bytes | None = None):
+    """Deterministic synthetic header blocks at dynamic table 0 (config 4's
+    shape; the qifs corpus itself is not available offline): per block a
+    uniform number of field lines, 30% indexed static, 40% static name
+    reference + value, 30% literal name + value; names and values are
+    alphabet-A text (nghttp3_amd/synth.py).  Returns (src, blocks, plain,
+    strs, lines, line_start)."""
+    from . import synth
+    alphabet = alphabet or synth.ALPHABET_A
+    rng = np.random.default_rng(seed)
+    nf = rng.integers(fields[0], fields[1] + 1, nblocks)
+    nl = int(nf.sum())
+    op = rng.choice(np.array([FL_INDEXED, FL_INDEXED_NAME, FL_LITERAL], dtype=np.uint8),
+                    p=[0.3, 0.4, 0.3], size=nl)
+    has_name = op == FL_LITERAL
+    has_value = op != FL_INDEXED
+    nlen = rng.integers(namelen[0], namelen[1] + 1, nl) * has_name
+    vlen = rng.integers(valuelen[0], valuelen[1] + 1, nl) * has_value
+    # strings in line order: name (if any) then value (if any)
+    per = np.stack([nlen, vlen], axis=1).reshape(-1)
+    present = np.stack([has_name, has_value], axis=1).reshape(-1)
+    slen = per[present].astype(np.uint32)
+    sidx = np.cumsum(present) - 1
+    strs = np.zeros(slen.size, dtype=SPAN_IN_DTYPE)
+    strs["len"] = slen
+    if slen.size:
+        strs["off"][1:] = np.cumsum(slen.astype(np.uint64))[:-1]
+    plain = synth.fill(seed, int(slen.sum(dtype=np.uint64)), alphabet)
+    lines = np.zeros(nl, dtype=FIELD_LINE_DTYPE)
+    lines["opcode"] = op
+    lines["index"] = rng.integers(0, 99, nl) * (op != FL_LITERAL)
+    lines["name"] = np.where(has_name, sidx.reshape(-1, 2)[:, 0], -1)
+    lines["value"] = np.where(has_value, sidx.reshape(-1, 2)[:, 1], -1)
+    line_start = np.zeros(nblocks + 1, dtype=np.uint32)
+    line_start[1:] = np.cumsum(nf)
+    src, blocks = write_sections(plain, strs, lines, line_start)
+    return src, blocks, plain, strs, lines, line_start
+
+
+class FieldSectionDecoder:
+    """Whole header blocks -> every string of every block, decoded.
+
+    The framing scan runs on the host (C); all Huffman strings of the batch
+    then go to the GPU in one qh_decode_batch.  Returns per string the
+    decoded bytes' (off, len, status) in one output buffer; raw (non-H)
+    strings are reported as spans into the input."""
+
+    def __init__(self, device: int = 0, codec: HuffmanBatchCodec | None = None):
+        self.codec = codec or HuffmanBatchCodec(device)
+
+    def decode_blocks(self, src, blocks):
+        src = _u8(src)
+        lines, spans, ls, ss, status = scan_blocks(src, blocks)
+        huff = (spans["flags"] & SPAN_HUFFMAN) != 0
+        hspans = np.ascontiguousarray(spans[huff])
+        if hspans.size:
+            dst, out = self.codec.decode_host(src, hspans)
+        else:
+            dst, out = np.zeros(1, np.uint8), np.zeros(0, SPAN_OUT_DTYPE)
+        # a Huffman error fails its whole block (qpack.c:3608-3609 -> -401)
+        bad = out["status"] != 0
+        if bad.any():
+            owner = np.searchsorted(ss, np.nonzero(huff)[0][bad], side="right") - 1
+            status[np.unique(owner)] = QH_ERR_QPACK_DECOMPRESSION_FAILED
+        return {"lines": lines, "spans": spans, "line_start": ls, "span_start": ss,
+                "status": status, "huffman": huff, "dst": dst, "out": out}

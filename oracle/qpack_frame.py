@@ -1,0 +1,230 @@
+"""TEST INFRASTRUCTURE ONLY: pure-Python restatement of nghttp3's QPACK
+field-line framing around the Huffman strings.
+
+Only tests/ may import this module, as the checker of
+nghttp3_amd/csrc/qh_qpack.c.  It restates (lib/nghttp3_qpack.c):
+
+* qpack_read_varint :2481-2543 (limit 2^62 - 1, lib/nghttp3_qpack.h:43);
+* nghttp3_qpack_decoder_read_request :3347-3800 with fin = 1 and the whole
+  section present: prefix :3369-3437, opcodes :3439-3495, size checks
+  :3575-3588 / :3661-3674, unfinished representation :3780-3784;
+* nghttp3_qpack_decoder_read_encoder :2815-3150 (opcodes :2837-2875);
+* nghttp3_qpack_put_varint(_len) :2643-2682 and the writers
+  qpack_encoder_write_indexed_name :1851-1896 /
+  qpack_encoder_write_literal :1944-2006.
+
+Pinned by the reference's own fuzz corpus file
+(fuzz/corpus/fuzz_qpackdecoder/netbsd-hq.out.256.100.1, committed as
+tests/golden/netbsd-hq.out.256.100.1): the survey's run of the compiled
+reference CLI decoded it into an 18-block, 217-line QIF (SURVEY.md
+section 8c; 199 field lines plus a blank line per block), and every literal field line in it was written by
+the reference encoder, so re-writing it must give the same bytes.
+
+Results are tuples: lines are (opcode, flags, index, name_span, value_span)
+and spans are (off, len, flags) with the C-ABI's constant values.
+"""
+from __future__ import annotations
+
+from . import encode as huff_encode, encode_count as huff_encode_count
+
+INT_MAX = (1 << 62) - 1
+MAX_NAMELEN = 256
+MAX_VALUELEN = 65536
+
+HEADER_TOO_LARGE = -109
+DECOMPRESSION_FAILED = -401
+ENCODER_STREAM_ERROR = -402
+_OVERFLOW = -108
+
+SPAN_HUFFMAN, SPAN_NAME = 1, 2
+FL_INDEXED, FL_INDEXED_PB, FL_INDEXED_NAME, FL_INDEXED_NAME_PB, FL_LITERAL = 1, 2, 3, 4, 5
+ES_INSERT_INDEXED, ES_INSERT, ES_SET_DTABLE_CAP, ES_DUPLICATE = 6, 7, 8, 9
+DYNAMIC, NEVER = 1, 2
+
+
+class _Truncated(Exception):
+    pass
+
+
+class _Fail(Exception):
+    def __init__(self, code):
+        self.code = code
+
+
+def read_varint(buf: bytes, pos: int, prefix: int):
+    """qpack.c:2481-2543 over a complete buffer -> (value, new_pos)."""
+    if pos >= len(buf):
+        raise _Truncated
+    k = (1 << prefix) - 1
+    if buf[pos] & k != k:
+        return buf[pos] & k, pos + 1
+    n, shift = k, 0
+    pos += 1
+    while pos < len(buf):
+        add = buf[pos] & 0x7F
+        if shift > 62 or (INT_MAX >> shift) < add:
+            raise _Fail(_OVERFLOW)
+        add <<= shift
+        if INT_MAX - add < n:
+            raise _Fail(_OVERFLOW)
+        n += add
+        if buf[pos] & 0x80 == 0:
+            return n, pos + 1
+        pos += 1
+        shift += 7
+    raise _Truncated
+
+
+def _read_string(buf, pos, prefix, limit, kind, base_off, spans, too_large, bad):
+    if pos >= len(buf):
+        raise _Truncated
+    h = SPAN_HUFFMAN if buf[pos] & (1 << prefix) else 0
+    try:
+        n, pos = read_varint(buf, pos, prefix)
+    except _Fail:
+        raise _Fail(bad)
+    if n > limit or (h and n * 8 // 5 > limit):
+        raise _Fail(too_large)
+    if len(buf) - pos < n:
+        raise _Truncated
+    spans.append((base_off + pos, n, h | kind))
+    return len(spans) - 1, pos + n
+
+
+def scan_field_section(buf: bytes, base_off: int = 0):
+    """-> (status, prefix (ricnt, sign, delta_base) or None, lines, spans)."""
+    lines, spans = [], []
+    bad, big = DECOMPRESSION_FAILED, HEADER_TOO_LARGE
+    try:
+        ricnt, pos = read_varint(buf, 0, 8)
+        if pos >= len(buf):
+            raise _Truncated
+        sign = 1 if buf[pos] & 0x80 else 0
+        dbase, pos = read_varint(buf, pos, 7)
+        prefix = (ricnt, sign, dbase)
+        while pos < len(buf):
+            b = buf[pos]
+            name = value = -1
+            index = 0
+            if b & 0x80:
+                op, fl, ip, has_idx, has_val = FL_INDEXED, 0 if b & 0x40 else DYNAMIC, 6, True, False
+            elif b & 0x40:
+                fl = (NEVER if b & 0x20 else 0) | (0 if b & 0x10 else DYNAMIC)
+                op, ip, has_idx, has_val = FL_INDEXED_NAME, 4, True, True
+            elif b & 0x20:
+                op, fl, ip, has_idx, has_val = FL_LITERAL, NEVER if b & 0x10 else 0, 3, False, True
+            elif b & 0x10:
+                op, fl, ip, has_idx, has_val = FL_INDEXED_PB, DYNAMIC, 4, True, False
+            else:
+                op, fl = FL_INDEXED_NAME_PB, DYNAMIC | (NEVER if b & 0x08 else 0)
+                ip, has_idx, has_val = 3, True, True
+            if has_idx:
+                try:
+                    index, pos = read_varint(buf, pos, ip)
+                except _Fail:
+                    raise _Fail(bad)
+            else:
+                name, pos = _read_string(buf, pos, 3, MAX_NAMELEN, SPAN_NAME, base_off, spans, big, bad)
+            if has_val:
+                value, pos = _read_string(buf, pos, 7, MAX_VALUELEN, 0, base_off, spans, big, bad)
+            lines.append((op, fl, index, name, value))
+    except _Truncated:
+        return bad, None, [], []
+    except _Fail as e:
+        return (bad if e.code == _OVERFLOW else e.code), None, [], []
+    return 0, prefix, lines, spans
+
+
+def scan_encoder_stream(buf: bytes, base_off: int = 0):
+    """-> (consumed bytes or error, instructions, spans); a trailing partial
+    instruction is not consumed."""
+    lines, spans = [], []
+    bad, big = ENCODER_STREAM_ERROR, HEADER_TOO_LARGE
+    pos = 0
+    while pos < len(buf):
+        b = buf[pos]
+        n_lines, n_spans = len(lines), len(spans)
+        try:
+            name = value = -1
+            index = 0
+            if b & 0x80:
+                op, fl = ES_INSERT_INDEXED, 0 if b & 0x40 else DYNAMIC
+                try:
+                    index, p = read_varint(buf, pos, 6)
+                except _Fail:
+                    raise _Fail(bad)
+                value, p = _read_string(buf, p, 7, MAX_VALUELEN, 0, base_off, spans, big, bad)
+            elif b & 0x40:
+                op, fl = ES_INSERT, 0
+                name, p = _read_string(buf, pos, 5, MAX_NAMELEN, SPAN_NAME, base_off, spans, big, bad)
+                value, p = _read_string(buf, p, 7, MAX_VALUELEN, 0, base_off, spans, big, bad)
+            else:
+                op = ES_SET_DTABLE_CAP if b & 0x20 else ES_DUPLICATE
+                fl = 0 if b & 0x20 else DYNAMIC
+                try:
+                    index, p = read_varint(buf, pos, 5)
+                except _Fail:
+                    raise _Fail(bad)
+        except _Truncated:
+            del lines[n_lines:], spans[n_spans:]
+            break
+        except _Fail as e:
+            del lines[n_lines:], spans[n_spans:]
+            return e.code, lines, spans
+        lines.append((op, fl, index, name, value))
+        pos = p
+    return pos, lines, spans
+
+
+def put_varint(n: int, prefix: int, fb: int = 0) -> bytes:
+    """qpack.c:2643-2682: first byte keeps fb's bits above the prefix."""
+    k = (1 << prefix) - 1
+    if n < k:
+        return bytes([(fb & ~k & 0xFF) | n])
+    out = [(fb & ~k & 0xFF) | k]
+    n -= k
+    while n >= 128:
+        out.append(0x80 | (n & 0x7F))
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _put_string(fb: int, prefix: int, s: bytes) -> bytes:
+    hlen = huff_encode_count(s)
+    if hlen < len(s):
+        return put_varint(hlen, prefix, fb | (1 << prefix)) + huff_encode(s)
+    return put_varint(len(s), prefix, fb) + s
+
+
+def write_indexed(fb: int, idx: int, prefix: int) -> bytes:
+    return put_varint(idx, prefix, fb)
+
+
+def write_indexed_name(fb: int, nameidx: int, prefix: int, value: bytes) -> bytes:
+    """qpack.c:1851-1896"""
+    return put_varint(nameidx, prefix, fb) + _put_string(0, 7, value)
+
+
+def write_literal(fb: int, prefix: int, name: bytes, value: bytes) -> bytes:
+    """qpack.c:1944-2006"""
+    return _put_string(fb, prefix, name) + _put_string(0, 7, value)
+
+
+def read_qif_out(data: bytes):
+    """Records of an interop-runner encoded file, as written by
+    examples/qpack_encode.cc and read by qpack_decode.cc:230-260:
+    u64 stream id (big endian), u32 length (big endian), payload.
+    Stream 0 is the encoder stream."""
+    recs, pos = [], 0
+    while pos < len(data):
+        if len(data) - pos < 12:
+            raise ValueError("truncated record header")
+        sid = int.from_bytes(data[pos:pos + 8], "big")
+        n = int.from_bytes(data[pos + 8:pos + 12], "big")
+        pos += 12
+        if len(data) - pos < n:
+            raise ValueError("truncated record")
+        recs.append((sid, pos, n))
+        pos += n
+    return recs
