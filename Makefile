@@ -30,12 +30,16 @@ $(LIBDIR)/qh_qpack.o: $(CSRC)/qh_qpack.c include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o
+$(LIBDIR)/qh_http.o: $(CSRC)/qh_http.c include/qhuff.h
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 # Static archive of the same two objects, for linking into libnghttp3 in
 # place of the reference's Huffman objects.
-$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o
+$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
 	rm -f $@
 	ar rcs $@ $^
 

@@ -292,6 +292,15 @@ def main():
             pos = torch.arange(h_plain, device=dev, dtype=torch.int64) - starts
             q_ok = bool((d_dst[rep_d + pos] == d_plain[rep_w + pos]).all())
             del d_plain, w_off, rep_d, rep_w, starts, pos
+        # fused-epilogue candidate: name / value validation over the decoded
+        # strings in HBM (qh_k_check_fields)
+        d_ck = torch.stack([d_out[:, 0], (d_out[:, 1] & 0xFFFFFFFF)
+                            | (torch.from_numpy(hs["flags"].astype(np.int64)).to(dev) << 32)], dim=1)
+        d_ver = torch.empty(hs.size, dtype=torch.int8, device=dev)
+        qp.check_fields_dev(codec, d_dst, d_ck, d_ver)
+        t_ck = reduce(timed(lambda: qp.check_fields_dev(codec, d_dst, d_ck, d_ver), args.steps),
+                      dist.ReduceOp.MAX if world > 1 else None)
+        n_valid = int(d_ver.sum().item())
         # host-memory path: scan + H2D + decode + D2H of this rank's blocks
         a = time.perf_counter()
         for _ in range(reps):
@@ -307,13 +316,16 @@ def main():
                   "gpu_decode_GiBps": round(h_all / t_qd / GIB, 2),
                   "gpu_decode_ms": round(t_qd * 1e3, 4),
                   "host_scan_GBps": round(blk_all / world / t_scan_max / 1e9, 3),
+                  "gpu_check_fields_ms": round(t_ck * 1e3, 4),
+                  "gpu_check_fields_GiBps": round(h_all / t_ck / GIB, 2),
+                  "valid_strings_rank0": n_valid,
                   "host_path_blocks_per_s": round(nb_all / t_qh, 1),
                   "host_path_GiBps_incl_scan_h2d_d2h": round(h_all / t_qh / GIB, 3),
                   "bit_exact": q_bad == 0,
                   "shape": "synthetic (nghttp3_amd/qpack.py synth_field_sections): 4-20 lines per "
                            "block, 30% indexed static, 40% static name ref, 30% literal name; "
                            "names 4-24 B, values 1-128 B, alphabet A; dtable 0"}
-        del d_src, d_sp, d_dst, d_out
+        del d_src, d_sp, d_dst, d_out, d_ck, d_ver
 
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None

@@ -99,6 +99,10 @@ EXPORTED_FUNCTIONS = (
     "qh_qpack_write_literal",
     "qh_qpack_literal_bound",
     "qh_qpack_write_sections",
+    # field validation (csrc/qh_http.c, csrc/qh_validate.inc)
+    "nghttp3_check_header_name",
+    "nghttp3_check_header_value",
+    "qh_check_fields_batch",
     "qh_ctx_enable_timing",
     "qh_ctx_kernel_times",
     "qh_synth_spans",

@@ -46,4 +46,5 @@
 #include "qh_enc_stream.inc" // encoder (default codes): streaming region rounds
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
+#include "qh_validate.inc"  // field name / value validation batch
 

@@ -75,6 +75,12 @@ def _load():
         lib.qh_qpack_literal_bound.restype = sz
         lib.qh_qpack_write_sections.argtypes = [vp, vp, vp, vp, sz, vp, vp, sz, vp]
         lib.qh_qpack_write_sections.restype = i32
+        lib.nghttp3_check_header_name.argtypes = [vp, sz]
+        lib.nghttp3_check_header_name.restype = i32
+        lib.nghttp3_check_header_value.argtypes = [vp, sz]
+        lib.nghttp3_check_header_value.restype = i32
+        lib.qh_check_fields_batch.argtypes = [vp, vp, vp, sz, vp, i32]
+        lib.qh_check_fields_batch.restype = i32
         _L = lib
     return _L
 
@@ -233,6 +239,40 @@ def synth_field_sections(seed: int, nblocks: int, fields=(4, 20), namelen=(4, 24
     return src, blocks, plain, strs, lines, line_start
 
 
+def check_header_name(name) -> int:
+    """nghttp3_check_header_name (lib/nghttp3_http.c:691-709)."""
+    a = _u8(name)
+    return _load().nghttp3_check_header_name(_vp(a), a.size)
+
+
+def check_header_value(value) -> int:
+    """nghttp3_check_header_value (lib/nghttp3_http.c:798-838)."""
+    a = _u8(value)
+    return _load().nghttp3_check_header_value(_vp(a), a.size)
+
+
+def check_fields_host(codec: HuffmanBatchCodec, src, spans):
+    """Batch validation of host strings on the GPU (qh_check_fields_batch):
+    spans' QH_SPAN_NAME flag selects the name check.  -> int8 verdicts."""
+    lib = _load()
+    src = _u8(src)
+    spans = np.ascontiguousarray(spans, dtype=SPAN_IN_DTYPE)
+    v = np.zeros(max(spans.size, 1), dtype=np.int8)
+    _lib.check(lib.qh_check_fields_batch(codec._ctx, _vp(src), _vp(spans), spans.size, _vp(v),
+                                         _lib.QH_WHERE_HOST), "qh_check_fields_batch")
+    return v[:spans.size]
+
+
+def check_fields_dev(codec: HuffmanBatchCodec, src, spans, verdict):
+    """Device-resident form: src uint8, spans int64 [n,2] (SPAN_IN layout),
+    verdict int8 [n] torch tensors; asynchronous on the codec stream."""
+    lib = _load()
+    _lib.check(lib.qh_check_fields_batch(codec._ctx, ctypes.c_void_p(src.data_ptr()),
+                                         ctypes.c_void_p(spans.data_ptr()), spans.shape[0],
+                                         ctypes.c_void_p(verdict.data_ptr()), _lib.QH_WHERE_DEVICE),
+               "qh_check_fields_batch")
+
+
 class FieldSectionDecoder:
     """Whole header blocks -> every string of every block, decoded.
 
@@ -258,5 +298,17 @@ class FieldSectionDecoder:
         if bad.any():
             owner = np.searchsorted(ss, np.nonzero(huff)[0][bad], side="right") - 1
             status[np.unique(owner)] = QH_ERR_QPACK_DECOMPRESSION_FAILED
+        # field name / value validation of every string (qpack.c hands the
+        # decoded nv to http.c:383-528, which checks it with
+        # nghttp3_check_header_name / _value): Huffman strings in the
+        # decode destination, raw ones in place
+        verdict = np.zeros(spans.size, dtype=np.int8)
+        if hspans.size:
+            dsp = np.zeros(hspans.size, dtype=SPAN_IN_DTYPE)
+            dsp["off"], dsp["len"] = out["off"], out["len"]
+            dsp["flags"] = hspans["flags"]
+            verdict[huff] = check_fields_host(self.codec, dst, dsp)
+        if (~huff).any():
+            verdict[~huff] = check_fields_host(self.codec, src, np.ascontiguousarray(spans[~huff]))
         return {"lines": lines, "spans": spans, "line_start": ls, "span_start": ss,
-                "status": status, "huffman": huff, "dst": dst, "out": out}
+                "status": status, "huffman": huff, "dst": dst, "out": out, "verdict": verdict}

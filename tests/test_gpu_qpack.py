@@ -89,3 +89,48 @@ def test_synthetic_sections_decode_on_gpu_with_corruption(dec):
             else:
                 got = bytes(src[spans["off"][k]:spans["off"][k] + spans["len"][k]])
             assert got == want
+
+
+def _check_cases():
+    from test_http_check import cases
+    return cases(0x5EED0F6, 4000)
+
+
+def test_check_fields_batch_host_and_device_match_scalar(dec):
+    import torch
+    strs = _check_cases()
+    flags = [qpack.SPAN_NAME if i % 2 else 0 for i in range(len(strs))]
+    # unaligned, back-to-back packing
+    src = np.frombuffer(b"\x01" * 3 + b"".join(strs), dtype=np.uint8)
+    spans = np.zeros(len(strs), dtype=SPAN_IN_DTYPE)
+    spans["len"] = [len(x) for x in strs]
+    spans["off"] = 3 + np.concatenate([[0], np.cumsum(spans["len"].astype(np.uint64))[:-1]])
+    spans["flags"] = flags
+    want = np.array([qpack.check_header_name(x) if f else qpack.check_header_value(x)
+                     for x, f in zip(strs, flags)], dtype=np.int8)
+    got = qpack.check_fields_host(dec.codec, src, spans)
+    assert (got == want).all()
+    # device-resident, padded buffer
+    d_src = torch.zeros(src.size + 64, dtype=torch.uint8, device="cuda")
+    d_src[:src.size] = torch.from_numpy(src.copy()).cuda()
+    d_sp = torch.from_numpy(spans.view(np.int64).reshape(-1, 2).copy()).cuda()
+    d_v = torch.full((len(strs),), -7, dtype=torch.int8, device="cuda")
+    qpack.check_fields_dev(dec.codec, d_src, d_sp, d_v)
+    torch.cuda.synchronize()
+    assert (d_v.cpu().numpy() == want).all()
+
+
+def test_decode_blocks_validates_every_string(dec):
+    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED0007, 512)
+    src = src.copy()
+    res = dec.decode_blocks(src, blocks)
+    assert (res["status"] == 0).all()
+    # synthetic names / values are alphabet A: upper-case letters make names
+    # invalid (nghttp3 rejects upper case), values are all valid
+    pb = bytes(plain)
+    names = (res["spans"]["flags"] & qpack.SPAN_NAME) != 0
+    ks = [int(k) for l in lines for k in (l["name"], l["value"]) if k >= 0]
+    for j, k in enumerate(ks):
+        s = pb[strs["off"][k]:strs["off"][k] + strs["len"][k]]
+        want = qpack.check_header_name(s) if names[j] else qpack.check_header_value(s)
+        assert res["verdict"][j] == want
