@@ -22,7 +22,7 @@ $(LIBDIR)/qh_scalar.o: $(CSRC)/qh_scalar.c $(CSRC)/qh_tables.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(CSRC)/qh_tables.h include/qhuff.h
+$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(CSRC)/qh_tables.h $(CSRC)/qh_tokens.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -30,7 +30,7 @@ $(LIBDIR)/qh_qpack.o: $(CSRC)/qh_qpack.c include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIBDIR)/qh_http.o: $(CSRC)/qh_http.c include/qhuff.h
+$(LIBDIR)/qh_http.o: $(CSRC)/qh_http.c $(CSRC)/qh_tokens.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 

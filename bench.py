@@ -301,6 +301,14 @@ def main():
         t_ck = reduce(timed(lambda: qp.check_fields_dev(codec, d_dst, d_ck, d_ver), args.steps),
                       dist.ReduceOp.MAX if world > 1 else None)
         n_valid = int(d_ver.sum().item())
+        # header-name tokens of the decoded names (qh_k_lookup_tokens, 8(f) row 4)
+        nm_mask = torch.from_numpy((hs["flags"] & qp.SPAN_NAME) != 0).to(dev)
+        d_nm = d_ck[nm_mask].contiguous()
+        d_tok = torch.empty(d_nm.shape[0], dtype=torch.int32, device=dev)
+        qp.lookup_tokens_dev(codec, d_dst, d_nm, d_tok)
+        t_tok = reduce(timed(lambda: qp.lookup_tokens_dev(codec, d_dst, d_nm, d_tok), args.steps),
+                       dist.ReduceOp.MAX if world > 1 else None)
+        n_names = int(d_nm.shape[0])
         # host-memory path: scan + H2D + decode + D2H of this rank's blocks
         a = time.perf_counter()
         for _ in range(reps):
@@ -319,13 +327,15 @@ def main():
                   "gpu_check_fields_ms": round(t_ck * 1e3, 4),
                   "gpu_check_fields_GiBps": round(h_all / t_ck / GIB, 2),
                   "valid_strings_rank0": n_valid,
+                  "gpu_lookup_tokens_ms": round(t_tok * 1e3, 4),
+                  "names_rank0": n_names,
                   "host_path_blocks_per_s": round(nb_all / t_qh, 1),
                   "host_path_GiBps_incl_scan_h2d_d2h": round(h_all / t_qh / GIB, 3),
                   "bit_exact": q_bad == 0,
                   "shape": "synthetic (nghttp3_amd/qpack.py synth_field_sections): 4-20 lines per "
                            "block, 30% indexed static, 40% static name ref, 30% literal name; "
                            "names 4-24 B, values 1-128 B, alphabet A; dtable 0"}
-        del d_src, d_sp, d_dst, d_out, d_ck, d_ver
+        del d_src, d_sp, d_dst, d_out, d_ck, d_ver, d_nm, d_tok
 
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None

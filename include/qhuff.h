@@ -357,6 +357,17 @@ QH_EXPORT int qh_check_fields_batch(qh_ctx *ctx, const uint8_t *src,
                                     const qh_span_in *in, size_t n,
                                     int8_t *verdict, int where);
 
+/* ---- Header-name tokens ------------------
+ * qh_qpack_lookup_token replaces the static qpack_lookup_token
+ * (lib/nghttp3_qpack.c:342, generated by genlibtokenlookup.py): the
+ * nghttp3_qpack_token of a field name (nghttp3.h:840-1131), or -1.  The
+ * batch form looks up every string of a batch on the GPU (names decoded by
+ * qh_decode_batch stay in HBM). */
+QH_EXPORT int32_t qh_qpack_lookup_token(const uint8_t *name, size_t namelen);
+QH_EXPORT int qh_lookup_tokens_batch(qh_ctx *ctx, const uint8_t *src,
+                                     const qh_span_in *in, size_t n,
+                                     int32_t *token, int where);
+
 /* Library version string. */
 QH_EXPORT const char *qh_version(void);
 

@@ -103,6 +103,9 @@ EXPORTED_FUNCTIONS = (
     "nghttp3_check_header_name",
     "nghttp3_check_header_value",
     "qh_check_fields_batch",
+    # header-name tokens (csrc/qh_http.c, csrc/qh_validate.inc)
+    "qh_qpack_lookup_token",
+    "qh_lookup_tokens_batch",
     "qh_ctx_enable_timing",
     "qh_ctx_kernel_times",
     "qh_synth_spans",

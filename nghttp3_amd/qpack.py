@@ -81,6 +81,10 @@ def _load():
         lib.nghttp3_check_header_value.restype = i32
         lib.qh_check_fields_batch.argtypes = [vp, vp, vp, sz, vp, i32]
         lib.qh_check_fields_batch.restype = i32
+        lib.qh_qpack_lookup_token.argtypes = [vp, sz]
+        lib.qh_qpack_lookup_token.restype = c.c_int32
+        lib.qh_lookup_tokens_batch.argtypes = [vp, vp, vp, sz, vp, i32]
+        lib.qh_lookup_tokens_batch.restype = i32
         _L = lib
     return _L
 
@@ -271,6 +275,33 @@ def check_fields_dev(codec: HuffmanBatchCodec, src, spans, verdict):
                                          ctypes.c_void_p(spans.data_ptr()), spans.shape[0],
                                          ctypes.c_void_p(verdict.data_ptr()), _lib.QH_WHERE_DEVICE),
                "qh_check_fields_batch")
+
+
+def lookup_token(name) -> int:
+    """qpack_lookup_token (lib/nghttp3_qpack.c:342): token or -1."""
+    a = _u8(name)
+    return _load().qh_qpack_lookup_token(_vp(a), a.size)
+
+
+def lookup_tokens_host(codec: HuffmanBatchCodec, src, spans):
+    """Batch token lookup on the GPU over host strings -> int32 tokens."""
+    lib = _load()
+    src = _u8(src)
+    spans = np.ascontiguousarray(spans, dtype=SPAN_IN_DTYPE)
+    t = np.zeros(max(spans.size, 1), dtype=np.int32)
+    _lib.check(lib.qh_lookup_tokens_batch(codec._ctx, _vp(src), _vp(spans), spans.size, _vp(t),
+                                          _lib.QH_WHERE_HOST), "qh_lookup_tokens_batch")
+    return t[:spans.size]
+
+
+def lookup_tokens_dev(codec: HuffmanBatchCodec, src, spans, token):
+    """Device-resident form (torch tensors: uint8 src, int64 [n,2] spans,
+    int32 [n] tokens); asynchronous on the codec stream."""
+    lib = _load()
+    _lib.check(lib.qh_lookup_tokens_batch(codec._ctx, ctypes.c_void_p(src.data_ptr()),
+                                          ctypes.c_void_p(spans.data_ptr()), spans.shape[0],
+                                          ctypes.c_void_p(token.data_ptr()), _lib.QH_WHERE_DEVICE),
+               "qh_lookup_tokens_batch")
 
 
 class FieldSectionDecoder:

@@ -29,3 +29,14 @@ def check_header_value(value: bytes, value_chars) -> int:
     if value[0] in ws or value[-1] in ws:
         return 0
     return int(all(value_chars[c] for c in value))
+
+
+def lookup_token(name: bytes, tokens) -> int:
+    """qpack_lookup_token (lib/nghttp3_qpack.c:342): exact, case-sensitive
+    match of the whole name against the reference's token names
+    (tests/golden/tokens.json, parsed from nghttp3.h's nghttp3_qpack_token),
+    else -1."""
+    try:
+        return tokens.get(name.decode("latin-1"), -1)
+    except Exception:
+        return -1

@@ -134,3 +134,23 @@ def test_decode_blocks_validates_every_string(dec):
         s = pb[strs["off"][k]:strs["off"][k] + strs["len"][k]]
         want = qpack.check_header_name(s) if names[j] else qpack.check_header_value(s)
         assert res["verdict"][j] == want
+
+
+def test_lookup_tokens_batch_host_and_device_match_scalar(dec):
+    import torch
+    from conftest import load_json
+    from test_http_check import token_cases
+    names = token_cases(load_json("tokens.json")["tokens"], 0x5EED0F8)
+    src = np.frombuffer(b"\x00" * 5 + b"".join(names), dtype=np.uint8)
+    spans = np.zeros(len(names), dtype=SPAN_IN_DTYPE)
+    spans["len"] = [len(x) for x in names]
+    spans["off"] = 5 + np.concatenate([[0], np.cumsum(spans["len"].astype(np.uint64))[:-1]])
+    want = np.array([qpack.lookup_token(x) for x in names], dtype=np.int32)
+    assert (want >= 0).sum() == 61
+    assert (qpack.lookup_tokens_host(dec.codec, src, spans) == want).all()
+    d_src = torch.from_numpy(src.copy()).cuda()
+    d_sp = torch.from_numpy(spans.view(np.int64).reshape(-1, 2).copy()).cuda()
+    d_t = torch.full((len(names),), -7, dtype=torch.int32, device="cuda")
+    qpack.lookup_tokens_dev(dec.codec, d_src, d_sp, d_t)
+    torch.cuda.synchronize()
+    assert (d_t.cpu().numpy() == want).all()

@@ -49,3 +49,23 @@ def test_scalar_checks_match_oracle(chars):
     for s in cases():
         assert qpack.check_header_name(s) == ref.check_header_name(s, names), s
         assert qpack.check_header_value(s) == ref.check_header_value(s, values), s
+
+
+def token_cases(tokens, seed=0x5EED0F7):
+    rng = random.Random(seed)
+    out = [b"", b":", b"x" * 33, b"x" * 32]
+    for k in tokens:
+        b = k.encode()
+        out += [b, b.upper(), b[:-1], b + b"x", b"x" + b[1:], b[:-1] + b"x", b[:1] + b"Z" + b[2:]]
+    for _ in range(2000):
+        out.append(bytes(rng.choice(b"abcdeghilmnoprstuvwxy-:") for _ in range(rng.randrange(1, 34))))
+    return out
+
+
+def test_lookup_token_matches_reference_enum():
+    tokens = load_json("tokens.json")["tokens"]
+    assert len(tokens) == 61
+    for name, tok in tokens.items():
+        assert qpack.lookup_token(name.encode()) == tok
+    for s in token_cases(tokens):
+        assert qpack.lookup_token(s) == ref.lookup_token(s, tokens), s
