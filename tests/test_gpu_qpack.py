@@ -146,7 +146,7 @@ def test_lookup_tokens_batch_host_and_device_match_scalar(dec):
     spans["len"] = [len(x) for x in names]
     spans["off"] = 5 + np.concatenate([[0], np.cumsum(spans["len"].astype(np.uint64))[:-1]])
     want = np.array([qpack.lookup_token(x) for x in names], dtype=np.int32)
-    assert (want >= 0).sum() == 61
+    assert (want >= 0).sum() >= 61  # every token name, plus random hits
     assert (qpack.lookup_tokens_host(dec.codec, src, spans) == want).all()
     d_src = torch.from_numpy(src.copy()).cuda()
     d_sp = torch.from_numpy(spans.view(np.int64).reshape(-1, 2).copy()).cuda()
