@@ -91,6 +91,7 @@ EXPORTED_FUNCTIONS = (
     # QPACK field-line framing (csrc/qh_qpack.c, bound in qpack.py)
     "qh_qpack_scan_field_section",
     "qh_qpack_scan_blocks",
+    "qh_scan_blocks_batch",
     "qh_qpack_scan_encoder_stream",
     "qh_qpack_put_varint_len",
     "qh_qpack_put_varint",

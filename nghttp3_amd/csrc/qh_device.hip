@@ -46,5 +46,6 @@
 #include "qh_enc_stream.inc" // encoder (default codes): streaming region rounds
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
-#include "qh_validate.inc"  // field name / value validation batch
+#include "qh_validate.inc"  // field name / value validation batch, header-name tokens
+#include "qh_frame.inc"     // QPACK field-section framing on the device
 

@@ -29,210 +29,13 @@
 
 #include "../../include/qhuff.h"
 
-#define QH_QPACK_INT_MAX ((1ull << 62) - 1) /* nghttp3_qpack.h:43 */
-#define QH_QPACK_MAX_NAMELEN 256            /* nghttp3_qpack.h:47 */
-#define QH_QPACK_MAX_VALUELEN 65536         /* nghttp3_qpack.h:50 */
-
-/* Reads an N-bit-prefix integer starting at *pp (the first byte's prefix
- * bits).  Returns 1 when complete, 0 when the input ends first, or
- * QH_ERR_QPACK_FATAL on overflow -- the same verdicts as
- * qpack_read_varint (qpack.c:2481-2543) given the whole input at once. */
-static int read_varint(uint64_t *res, const uint8_t **pp, const uint8_t *end,
-                       unsigned prefix) {
-  const uint8_t *p = *pp;
-  uint64_t k = (uint8_t)((1u << prefix) - 1);
-  uint64_t n, add;
-  unsigned shift = 0;
-
-  if (p == end) {
-    return 0;
-  }
-  if ((*p & k) != k) {
-    *res = *p & k;
-    *pp = p + 1;
-    return 1;
-  }
-  n = k;
-  for (++p; p != end; ++p, shift += 7) {
-    add = *p & 0x7fu;
-    if (shift > 62) {
-      return QH_ERR_QPACK_FATAL;
-    }
-    if ((QH_QPACK_INT_MAX >> shift) < add) {
-      return QH_ERR_QPACK_FATAL;
-    }
-    add <<= shift;
-    if (QH_QPACK_INT_MAX - add < n) {
-      return QH_ERR_QPACK_FATAL;
-    }
-    n += add;
-    if ((*p & 0x80u) == 0) {
-      *res = n;
-      *pp = p + 1;
-      return 1;
-    }
-  }
-  return 0;
-}
-
-typedef struct scan_out {
-  qh_field_line *lines;
-  size_t lines_cap, nlines;
-  qh_span_in *spans;
-  size_t spans_cap, nspans;
-} scan_out;
-
-/* One string literal: H bit at bit `prefix` of the first byte, then the
- * prefixed length, then the bytes.  Checks the decoder's size limits on
- * the (estimated, for Huffman) decoded length (qpack.c:3575-3588,
- * :3661-3674).  Returns 1, 0 (truncated), or a negative error. */
-static int read_string(scan_out *o, int32_t *span_idx, const uint8_t *base,
-                       uint64_t base_off, const uint8_t **pp,
-                       const uint8_t *end, unsigned prefix, uint64_t limit,
-                       uint32_t kind, int too_large_rv, int bad_rv) {
-  const uint8_t *p = *pp;
-  uint64_t len;
-  uint32_t h;
-  int rv;
-  qh_span_in *s;
-
-  if (p == end) {
-    return 0;
-  }
-  h = (*p & (1u << prefix)) ? QH_SPAN_HUFFMAN : 0;
-  rv = read_varint(&len, &p, end, prefix);
-  if (rv < 0) {
-    return bad_rv;
-  }
-  if (rv == 0) {
-    return 0;
-  }
-  if (len > limit) {
-    return too_large_rv;
-  }
-  if (h && len * 8 / 5 > limit) { /* nghttp3_qpack_huffman.h:113-115 */
-    return too_large_rv;
-  }
-  if ((uint64_t)(end - p) < len) {
-    return 0;
-  }
-  if (o->nspans == o->spans_cap) {
-    return QH_ERR_NOMEM;
-  }
-  s = &o->spans[o->nspans];
-  s->off = base_off + (uint64_t)(p - base);
-  s->len = (uint32_t)len;
-  s->flags = h | kind;
-  *span_idx = (int32_t)o->nspans++;
-  *pp = p + len;
-  return 1;
-}
-
-static qh_field_line *new_line(scan_out *o, uint8_t opcode, uint8_t flags) {
-  qh_field_line *l;
-  if (o->nlines == o->lines_cap) {
-    return NULL;
-  }
-  l = &o->lines[o->nlines++];
-  memset(l, 0, sizeof(*l));
-  l->opcode = opcode;
-  l->flags = flags;
-  l->name = -1;
-  l->value = -1;
-  return l;
-}
-
-static int scan_section(scan_out *o, const uint8_t *src, size_t srclen,
-                        uint64_t src_off, qh_section_prefix *prefix) {
-  const uint8_t *p = src, *end = src + srclen;
-  const int bad = QH_ERR_QPACK_DECOMPRESSION_FAILED;
-  const int big = QH_ERR_QPACK_HEADER_TOO_LARGE;
-  qh_section_prefix pf;
-  int rv;
-
-  /* Section prefix, qpack.c:3369-3437: Required Insert Count (8-bit
-   * prefix), then sign bit + Delta Base (7-bit prefix). */
-  rv = read_varint(&pf.ricnt, &p, end, 8);
-  if (rv <= 0) {
-    return bad;
-  }
-  if (p == end) {
-    return bad;
-  }
-  pf.sign = (*p & 0x80u) ? 1 : 0;
-  pf.reserved = 0;
-  rv = read_varint(&pf.delta_base, &p, end, 7);
-  if (rv <= 0) {
-    return bad;
-  }
-  if (prefix) {
-    *prefix = pf;
-  }
-
-  while (p != end) {
-    uint8_t b = *p, opcode, flags = 0;
-    unsigned iprefix;
-    int has_name_idx = 1, has_value = 1;
-    qh_field_line *l;
-
-    /* qpack.c:3439-3495 */
-    if (b & 0x80u) {
-      opcode = QH_FL_INDEXED;
-      flags = (b & 0x40u) ? 0 : QH_FL_DYNAMIC;
-      iprefix = 6;
-      has_value = 0;
-    } else if (b & 0x40u) {
-      opcode = QH_FL_INDEXED_NAME;
-      flags = (uint8_t)(((b & 0x20u) ? QH_FL_NEVER : 0) |
-                        ((b & 0x10u) ? 0 : QH_FL_DYNAMIC));
-      iprefix = 4;
-    } else if (b & 0x20u) {
-      opcode = QH_FL_LITERAL;
-      flags = (b & 0x10u) ? QH_FL_NEVER : 0;
-      iprefix = 3;
-      has_name_idx = 0;
-    } else if (b & 0x10u) {
-      opcode = QH_FL_INDEXED_PB;
-      flags = QH_FL_DYNAMIC;
-      iprefix = 4;
-      has_value = 0;
-    } else {
-      opcode = QH_FL_INDEXED_NAME_PB;
-      flags = (uint8_t)(QH_FL_DYNAMIC | ((b & 0x08u) ? QH_FL_NEVER : 0));
-      iprefix = 3;
-    }
-    l = new_line(o, opcode, flags);
-    if (l == NULL) {
-      return QH_ERR_NOMEM;
-    }
-    if (has_name_idx) {
-      rv = read_varint(&l->index, &p, end, iprefix);
-      if (rv <= 0) {
-        return bad; /* overflow, or unfinished at fin (:3780-3784) */
-      }
-    } else {
-      rv = read_string(o, &l->name, src, src_off, &p, end, 3,
-                       QH_QPACK_MAX_NAMELEN, QH_SPAN_NAME, big, bad);
-      if (rv <= 0) {
-        return rv < 0 ? rv : bad;
-      }
-    }
-    if (has_value) {
-      rv = read_string(o, &l->value, src, src_off, &p, end, 7,
-                       QH_QPACK_MAX_VALUELEN, 0, big, bad);
-      if (rv <= 0) {
-        return rv < 0 ? rv : bad;
-      }
-    }
-  }
-  return 0;
-}
+#include "qh_qpack_core.h"
 
 QH_EXPORT int qh_qpack_scan_field_section(
   const uint8_t *src, size_t srclen, uint64_t src_off,
   qh_section_prefix *prefix, qh_field_line *lines, size_t lines_cap,
   size_t *nlines, qh_span_in *spans, size_t spans_cap, size_t *nspans) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0};
+  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}};
   int rv;
 
   if ((src == NULL && srclen) || nlines == NULL || nspans == NULL ||
@@ -251,7 +54,7 @@ QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
                                    qh_span_in *spans, size_t spans_cap,
                                    uint32_t *line_start, uint32_t *span_start,
                                    int32_t *status) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0};
+  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}};
   size_t i;
 
   if ((src == NULL && nblocks) || (blocks == NULL && nblocks) ||
@@ -287,7 +90,7 @@ QH_EXPORT nghttp3_ssize qh_qpack_scan_encoder_stream(
   const uint8_t *src, size_t srclen, uint64_t src_off, qh_field_line *insts,
   size_t insts_cap, size_t *ninsts, qh_span_in *spans, size_t spans_cap,
   size_t *nspans) {
-  scan_out o = {insts, insts_cap, 0, spans, spans_cap, 0};
+  scan_out o = {insts, insts_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}};
   const uint8_t *p = src, *end = src + srclen, *done = src;
   const int bad = QH_ERR_QPACK_ENCODER_STREAM_ERROR;
   const int big = QH_ERR_QPACK_HEADER_TOO_LARGE; /* qpack.c:2962-2972 */

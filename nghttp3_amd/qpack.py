@@ -81,6 +81,8 @@ def _load():
         lib.nghttp3_check_header_value.restype = i32
         lib.qh_check_fields_batch.argtypes = [vp, vp, vp, sz, vp, i32]
         lib.qh_check_fields_batch.restype = i32
+        lib.qh_scan_blocks_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp, vp, i32]
+        lib.qh_scan_blocks_batch.restype = i32
         lib.qh_qpack_lookup_token.argtypes = [vp, sz]
         lib.qh_qpack_lookup_token.restype = c.c_int32
         lib.qh_lookup_tokens_batch.argtypes = [vp, vp, vp, sz, vp, i32]
@@ -134,6 +136,19 @@ def scan_blocks(src, blocks):
     _lib.check(lib.qh_qpack_scan_blocks(_vp(src), _vp(blocks), nb, _vp(lines), cap, _vp(spans), cap,
                                         _vp(ls), _vp(ss), _vp(st)), "qh_qpack_scan_blocks")
     return lines[:ls[nb]], spans[:ss[nb]], ls, ss, st[:nb]
+
+
+def scan_blocks_dev(codec: HuffmanBatchCodec, src, blocks, lines, spans, line_start, span_start,
+                    status):
+    """GPU framing (qh_scan_blocks_batch) over torch tensors in HBM: src
+    uint8, blocks int64 [n,2] (SPAN_IN layout), lines uint8 [cap*24], spans
+    int64 [cap,2], line_start / span_start int32 [n+1], status int32 [n]."""
+    lib = _load()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    _lib.check(lib.qh_scan_blocks_batch(codec._ctx, p(src), p(blocks), blocks.shape[0], p(lines),
+                                        lines.numel() // FIELD_LINE_DTYPE.itemsize, p(spans),
+                                        spans.shape[0], p(line_start), p(span_start), p(status),
+                                        _lib.QH_WHERE_DEVICE), "qh_scan_blocks_batch")
 
 
 def scan_encoder_stream(buf, base_off: int = 0):

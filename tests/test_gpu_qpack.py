@@ -154,3 +154,50 @@ def test_lookup_tokens_batch_host_and_device_match_scalar(dec):
     qpack.lookup_tokens_dev(dec.codec, d_src, d_sp, d_t)
     torch.cuda.synchronize()
     assert (d_t.cpu().numpy() == want).all()
+
+
+def _gpu_scan(dec, src, blocks):
+    import torch
+    n = blocks.size
+    cap = int(blocks["len"].sum(dtype=np.uint64)) + 1
+    d_src = torch.from_numpy(np.ascontiguousarray(src)).cuda()
+    d_blk = torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda()
+    d_lines = torch.zeros(cap * qpack.FIELD_LINE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    d_spans = torch.zeros((cap, 2), dtype=torch.int64, device="cuda")
+    d_ls = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    d_ss = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    d_st = torch.full((max(n, 1),), 7, dtype=torch.int32, device="cuda")
+    qpack.scan_blocks_dev(dec.codec, d_src, d_blk, d_lines, d_spans, d_ls, d_ss, d_st)
+    torch.cuda.synchronize()
+    ls = d_ls.cpu().numpy().view(np.uint32)
+    ss = d_ss.cpu().numpy().view(np.uint32)
+    lines = d_lines.cpu().numpy().view(qpack.FIELD_LINE_DTYPE)[:ls[n]]
+    spans = d_spans.cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1)[:ss[n]]
+    return lines, spans, ls, ss, d_st.cpu().numpy()[:n]
+
+
+def _same_scan(a, b):
+    for x, y in zip(a, b):
+        assert x.shape == y.shape
+        assert x.tobytes() == y.tobytes()
+
+
+def test_gpu_framing_matches_host_scan_on_netbsd_and_synthetic(dec):
+    data = open(os.path.join(GOLDEN, "netbsd-hq.out.256.100.1"), "rb").read()
+    recs = [r for r in ref.read_qif_out(data) if r[0] != 0]
+    blocks = np.zeros(len(recs), dtype=SPAN_IN_DTYPE)
+    blocks["off"] = [r[1] for r in recs]
+    blocks["len"] = [r[2] for r in recs]
+    src = np.frombuffer(data, dtype=np.uint8)
+    _same_scan(_gpu_scan(dec, src, blocks), qpack.scan_blocks(src, blocks))
+    # synthetic batch with failing blocks (truncations, overflow, too large)
+    src, blocks, *_ = qpack.synth_field_sections(0x5EED0009, 5000)
+    src = src.copy()
+    blocks = blocks.copy()
+    blocks["len"][10] -= 1
+    blocks["len"][11] = 1
+    src[blocks["off"][12] + 2] = 0x2F
+    src[blocks["off"][12] + 3:blocks["off"][12] + 16] = 0xFF
+    _same_scan(_gpu_scan(dec, src, blocks), qpack.scan_blocks(src, blocks))
+    st = _gpu_scan(dec, src, blocks)[4]
+    assert (st[[10, 11, 12]] != 0).all() and (st[:10] == 0).all()
