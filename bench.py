@@ -292,6 +292,20 @@ def main():
             pos = torch.arange(h_plain, device=dev, dtype=torch.int64) - starts
             q_ok = bool((d_dst[rep_d + pos] == d_plain[rep_w + pos]).all())
             del d_plain, w_off, rep_d, rep_w, starts, pos
+        # framing on the device too (qh_scan_blocks_batch, same parser source)
+        g_blk = torch.from_numpy(my.view(np.int64).reshape(-1, 2).copy()).to(dev)
+        g_cap = int(q_host.size) + 1
+        g_lines = torch.empty(g_cap * qp.FIELD_LINE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        g_spans = torch.empty((g_cap, 2), dtype=torch.int64, device=dev)
+        g_ls = torch.empty(my.size + 1, dtype=torch.int32, device=dev)
+        g_ss = torch.empty(my.size + 1, dtype=torch.int32, device=dev)
+        g_st = torch.empty(my.size, dtype=torch.int32, device=dev)
+        g_scan = lambda: qp.scan_blocks_dev(codec, d_src, g_blk, g_lines, g_spans, g_ls, g_ss, g_st)
+        g_scan()
+        t_gscan = reduce(timed(g_scan, args.steps), dist.ReduceOp.MAX if world > 1 else None)
+        g_ok = int(g_ss[-1].item()) == q_sp.size and bool((g_st == 0).all()) and \
+            bool((g_spans[:q_sp.size].cpu().numpy().view(q.SPAN_IN_DTYPE).reshape(-1) == q_sp).all())
+        del g_blk, g_lines, g_spans, g_ls, g_ss, g_st
         # fused-epilogue candidate: name / value validation over the decoded
         # strings in HBM (qh_k_check_fields)
         d_ck = torch.stack([d_out[:, 0], (d_out[:, 1] & 0xFFFFFFFF)
@@ -324,6 +338,9 @@ def main():
                   "gpu_decode_GiBps": round(h_all / t_qd / GIB, 2),
                   "gpu_decode_ms": round(t_qd * 1e3, 4),
                   "host_scan_GBps": round(blk_all / world / t_scan_max / 1e9, 3),
+                  "gpu_scan_ms": round(t_gscan * 1e3, 4),
+                  "gpu_scan_GBps": round(blk_all / t_gscan / 1e9, 2),
+                  "gpu_scan_matches_host": g_ok,
                   "gpu_check_fields_ms": round(t_ck * 1e3, 4),
                   "gpu_check_fields_GiBps": round(h_all / t_ck / GIB, 2),
                   "valid_strings_rank0": n_valid,
