@@ -323,6 +323,15 @@ def main():
         t_tok = reduce(timed(lambda: qp.lookup_tokens_dev(codec, d_dst, d_nm, d_tok), args.steps),
                        dist.ReduceOp.MAX if world > 1 else None)
         n_names = int(d_nm.shape[0])
+        # whole device-resident block pipeline: frame + decode + validate + tokens
+        fsd = qp.FieldSectionDecoder(codec=codec)
+        p_blk = torch.from_numpy(my.view(np.int64).reshape(-1, 2).copy()).to(dev)
+        p_bufs = fsd.decode_blocks_dev(d_src, p_blk)
+        p_ok = bool(torch.equal(p_bufs["out"], d_out)) and \
+            bool(torch.equal(p_bufs["verdict"], d_ver)) and bool(torch.equal(p_bufs["tokens"], d_tok))
+        t_pipe = reduce(timed(lambda: fsd.decode_blocks_dev(d_src, p_blk, p_bufs), args.steps),
+                        dist.ReduceOp.MAX if world > 1 else None)
+        del p_blk, p_bufs
         # host-memory path: scan + H2D + decode + D2H of this rank's blocks
         a = time.perf_counter()
         for _ in range(reps):
@@ -341,6 +350,10 @@ def main():
                   "gpu_scan_ms": round(t_gscan * 1e3, 4),
                   "gpu_scan_GBps": round(blk_all / t_gscan / 1e9, 2),
                   "gpu_scan_matches_host": g_ok,
+                  "gpu_pipeline_ms": round(t_pipe * 1e3, 4),
+                  "gpu_pipeline_blocks_per_s": round(nb_all / t_pipe, 1),
+                  "gpu_pipeline_GiBps": round(h_all / t_pipe / GIB, 2),
+                  "gpu_pipeline_matches_staged": p_ok,
                   "gpu_check_fields_ms": round(t_ck * 1e3, 4),
                   "gpu_check_fields_GiBps": round(h_all / t_ck / GIB, 2),
                   "valid_strings_rank0": n_valid,

@@ -330,6 +330,49 @@ class FieldSectionDecoder:
     def __init__(self, device: int = 0, codec: HuffmanBatchCodec | None = None):
         self.codec = codec or HuffmanBatchCodec(device)
 
+    def decode_blocks_dev(self, src, blocks, bufs=None):
+        """Device-resident pipeline: header blocks already in HBM (src uint8,
+        blocks int64 [n,2]) -> GPU framing, decode of every Huffman string,
+        validation of every Huffman-coded name / value and tokens of those
+        names, with no host round trip of string data (one small sync in
+        the framing call).  Returns a dict of torch tensors; `bufs` (the
+        dict of a previous call) reuses its allocations."""
+        import torch
+        dev = src.device
+        n = blocks.shape[0]
+        b = bufs or {}
+        cap = int(src.numel()) + 1
+        if b.get("cap", -1) < cap or b.get("n", -1) < n:
+            b = {"cap": cap, "n": n,
+                 "lines": torch.empty(cap * FIELD_LINE_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+                 "spans": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "line_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
+                 "span_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
+                 "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev)}
+        scan_blocks_dev(self.codec, src, blocks, b["lines"], b["spans"], b["line_start"][:n + 1],
+                        b["span_start"][:n + 1], b["status"][:n])
+        ns = int(b["span_start"][n].item())
+        spans = b["spans"][:ns]
+        flags = spans[:, 1] >> 32
+        hsel = (flags & SPAN_HUFFMAN) != 0
+        hs = spans[hsel].contiguous()
+        slots = (hs[:, 1] & 0xFFFFFFFF) * 8 // 5 + 16
+        cap_d = int(((slots + 63) // 64 * 64).sum().item())
+        dst = torch.empty(max(cap_d, 1), dtype=torch.uint8, device=dev)
+        out = torch.empty((hs.shape[0], 2), dtype=torch.int64, device=dev)
+        if hs.shape[0]:
+            self.codec.decode_dev(src, hs, dst, out)
+        ck = torch.stack([out[:, 0], (out[:, 1] & 0xFFFFFFFF) | ((hs[:, 1] >> 32) << 32)], dim=1)
+        verdict = torch.empty(hs.shape[0], dtype=torch.int8, device=dev)
+        check_fields_dev(self.codec, dst, ck, verdict)
+        nsel = ((hs[:, 1] >> 32) & SPAN_NAME) != 0
+        names = ck[nsel].contiguous()
+        tokens = torch.empty(names.shape[0], dtype=torch.int32, device=dev)
+        lookup_tokens_dev(self.codec, dst, names, tokens)
+        b.update({"nspans": ns, "huffman": hsel, "hspans": hs, "dst": dst, "out": out,
+                  "verdict": verdict, "name_sel": nsel, "tokens": tokens})
+        return b
+
     def decode_blocks(self, src, blocks):
         src = _u8(src)
         lines, spans, ls, ss, status = scan_blocks(src, blocks)

@@ -201,3 +201,24 @@ def test_gpu_framing_matches_host_scan_on_netbsd_and_synthetic(dec):
     _same_scan(_gpu_scan(dec, src, blocks), qpack.scan_blocks(src, blocks))
     st = _gpu_scan(dec, src, blocks)[4]
     assert (st[[11, 12]] == qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED).all() and (st[:10] == 0).all()
+
+
+def test_device_pipeline_matches_staged_path(dec):
+    import torch
+    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED000A, 3000)
+    res = dec.decode_blocks(src, blocks)
+    d = dec.decode_blocks_dev(torch.from_numpy(np.ascontiguousarray(src)).cuda(),
+                              torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+    torch.cuda.synchronize()
+    assert (d["status"][:blocks.size].cpu().numpy() == res["status"]).all()
+    assert d["nspans"] == res["spans"].size
+    out = d["out"].cpu().numpy()
+    dst = d["dst"].cpu().numpy()
+    ho = res["out"]
+    for k in range(ho.size):
+        a = bytes(res["dst"][ho["off"][k]:ho["off"][k] + ho["len"][k]])
+        b = bytes(dst[out[k, 0]:out[k, 0] + (out[k, 1] & 0xFFFFFFFF)])
+        assert a == b
+    assert (d["verdict"].cpu().numpy() == res["verdict"][res["huffman"]]).all()
+    names = [bytes(dst[o:o + (l & 0xFFFFFFFF)]) for o, l in out[d["name_sel"].cpu().numpy()]]
+    assert (d["tokens"].cpu().numpy() == [qpack.lookup_token(x) for x in names]).all()
