@@ -327,8 +327,10 @@ def main():
         fsd = qp.FieldSectionDecoder(codec=codec)
         p_blk = torch.from_numpy(my.view(np.int64).reshape(-1, 2).copy()).to(dev)
         p_bufs = fsd.decode_blocks_dev(d_src, p_blk)
-        p_ok = bool(torch.equal(p_bufs["out"], d_out)) and \
-            bool(torch.equal(p_bufs["verdict"], d_ver)) and bool(torch.equal(p_bufs["tokens"], d_tok))
+        p_nh = p_bufs["nhuff"]
+        p_ok = p_nh == hs.size and bool(torch.equal(p_bufs["out"][:p_nh], d_out)) and \
+            bool(torch.equal(p_bufs["verdict"][:p_nh], d_ver)) and \
+            bool(torch.equal(p_bufs["tokens"][:p_nh][p_bufs["name_sel"]], d_tok))
         t_pipe = reduce(timed(lambda: fsd.decode_blocks_dev(d_src, p_blk, p_bufs), args.steps),
                         dist.ReduceOp.MAX if world > 1 else None)
         del p_blk, p_bufs

@@ -290,16 +290,20 @@ QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
                                    int32_t *status);
 
 /* The same batch scan on the GPU (blocks, lines, spans, line_start,
- * span_start and status all in HBM; where must be QH_WHERE_DEVICE): same
- * parser source, same outputs and verdicts as qh_qpack_scan_blocks.
- * Synchronises once (to check the totals against the caps); returns 0,
- * QH_ERR_NOMEM or QH_ERR_FATAL. */
+ * span_start, status and huff in HBM; where must be QH_WHERE_DEVICE): same
+ * parser source, same outputs and verdicts as qh_qpack_scan_blocks.  If
+ * huff is not NULL it also receives the Huffman-coded spans alone, in
+ * order, ready for qh_decode_batch.  totals (host, may be NULL) receives
+ * {lines, spans, Huffman spans}.  Synchronises once (to check the totals
+ * against the caps); returns 0, QH_ERR_NOMEM or QH_ERR_FATAL. */
 QH_EXPORT int qh_scan_blocks_batch(qh_ctx *ctx, const uint8_t *src,
                                    const qh_span_in *blocks, size_t nblocks,
                                    qh_field_line *lines, size_t lines_cap,
                                    qh_span_in *spans, size_t spans_cap,
                                    uint32_t *line_start, uint32_t *span_start,
-                                   int32_t *status, int where);
+                                   int32_t *status, qh_span_in *huff,
+                                   size_t huff_cap, uint64_t *totals,
+                                   int where);
 
 /* Scans encoder-stream bytes.  Returns the number of bytes of complete
  * instructions (a trailing partial instruction is left for the next call,

@@ -64,6 +64,7 @@ typedef struct scan_out {
   qh_span_in *spans;
   size_t spans_cap, nspans;
   qh_field_line scratch;
+  size_t nhuff; /* Huffman-coded strings seen */
 } scan_out;
 
 /* One string literal: H bit at bit `prefix` of the first byte, then the
@@ -110,6 +111,7 @@ QH_HD static inline int read_string(scan_out *o, int32_t *span_idx, const uint8_
     s->flags = h | kind;
   }
   *span_idx = (int32_t)o->nspans++;
+  o->nhuff += h ? 1 : 0;
   *pp = p + len;
   return 1;
 }

@@ -81,7 +81,8 @@ def _load():
         lib.nghttp3_check_header_value.restype = i32
         lib.qh_check_fields_batch.argtypes = [vp, vp, vp, sz, vp, i32]
         lib.qh_check_fields_batch.restype = i32
-        lib.qh_scan_blocks_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp, vp, i32]
+        lib.qh_scan_blocks_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp, vp, vp, sz,
+                                             c.POINTER(c.c_uint64), i32]
         lib.qh_scan_blocks_batch.restype = i32
         lib.qh_qpack_lookup_token.argtypes = [vp, sz]
         lib.qh_qpack_lookup_token.restype = c.c_int32
@@ -139,16 +140,21 @@ def scan_blocks(src, blocks):
 
 
 def scan_blocks_dev(codec: HuffmanBatchCodec, src, blocks, lines, spans, line_start, span_start,
-                    status):
+                    status, huff=None):
     """GPU framing (qh_scan_blocks_batch) over torch tensors in HBM: src
     uint8, blocks int64 [n,2] (SPAN_IN layout), lines uint8 [cap*24], spans
-    int64 [cap,2], line_start / span_start int32 [n+1], status int32 [n]."""
+    int64 [cap,2], line_start / span_start int32 [n+1], status int32 [n],
+    optional huff int64 [cap,2] (the Huffman spans alone).  Returns the
+    totals (lines, spans, Huffman spans)."""
     lib = _load()
-    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    tot = (ctypes.c_uint64 * 3)()
     _lib.check(lib.qh_scan_blocks_batch(codec._ctx, p(src), p(blocks), blocks.shape[0], p(lines),
                                         lines.numel() // FIELD_LINE_DTYPE.itemsize, p(spans),
                                         spans.shape[0], p(line_start), p(span_start), p(status),
+                                        p(huff), 0 if huff is None else huff.shape[0], tot,
                                         _lib.QH_WHERE_DEVICE), "qh_scan_blocks_batch")
+    return tot[0], tot[1], tot[2]
 
 
 def scan_encoder_stream(buf, base_off: int = 0):
@@ -343,34 +349,33 @@ class FieldSectionDecoder:
         b = bufs or {}
         cap = int(src.numel()) + 1
         if b.get("cap", -1) < cap or b.get("n", -1) < n:
+            # every line and string takes at least one byte of the blocks;
+            # a decode slot is at most len * 8 / 5 + 16 rounded up to 64
             b = {"cap": cap, "n": n,
                  "lines": torch.empty(cap * FIELD_LINE_DTYPE.itemsize, dtype=torch.uint8, device=dev),
                  "spans": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "hspans": torch.empty((cap, 2), dtype=torch.int64, device=dev),
                  "line_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
                  "span_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
-                 "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev)}
-        scan_blocks_dev(self.codec, src, blocks, b["lines"], b["spans"], b["line_start"][:n + 1],
-                        b["span_start"][:n + 1], b["status"][:n])
-        ns = int(b["span_start"][n].item())
-        spans = b["spans"][:ns]
-        flags = spans[:, 1] >> 32
-        hsel = (flags & SPAN_HUFFMAN) != 0
-        hs = spans[hsel].contiguous()
-        slots = (hs[:, 1] & 0xFFFFFFFF) * 8 // 5 + 16
-        cap_d = int(((slots + 63) // 64 * 64).sum().item())
-        dst = torch.empty(max(cap_d, 1), dtype=torch.uint8, device=dev)
-        out = torch.empty((hs.shape[0], 2), dtype=torch.int64, device=dev)
-        if hs.shape[0]:
-            self.codec.decode_dev(src, hs, dst, out)
-        ck = torch.stack([out[:, 0], (out[:, 1] & 0xFFFFFFFF) | ((hs[:, 1] >> 32) << 32)], dim=1)
-        verdict = torch.empty(hs.shape[0], dtype=torch.int8, device=dev)
-        check_fields_dev(self.codec, dst, ck, verdict)
-        nsel = ((hs[:, 1] >> 32) & SPAN_NAME) != 0
-        names = ck[nsel].contiguous()
-        tokens = torch.empty(names.shape[0], dtype=torch.int32, device=dev)
-        lookup_tokens_dev(self.codec, dst, names, tokens)
-        b.update({"nspans": ns, "huffman": hsel, "hspans": hs, "dst": dst, "out": out,
-                  "verdict": verdict, "name_sel": nsel, "tokens": tokens})
+                 "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                 "dst": torch.empty(cap * 8 // 5 + 79 * cap + 64, dtype=torch.uint8, device=dev),
+                 "out": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "ck": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "verdict": torch.empty(cap, dtype=torch.int8, device=dev),
+                 "tokens": torch.empty(cap, dtype=torch.int32, device=dev)}
+        _, ns, nh = scan_blocks_dev(self.codec, src, blocks, b["lines"], b["spans"],
+                                    b["line_start"][:n + 1], b["span_start"][:n + 1],
+                                    b["status"][:n], b["hspans"])
+        hs, out, ck = b["hspans"][:nh], b["out"][:nh], b["ck"][:nh]
+        if nh:
+            self.codec.decode_dev(src, hs, b["dst"], out)
+        # check / token spans: decoded (off, len) with the scanned flags
+        ck[:, 0] = out[:, 0]
+        ck[:, 1] = (out[:, 1] & 0xFFFFFFFF) | ((hs[:, 1] >> 32) << 32)
+        check_fields_dev(self.codec, b["dst"], ck, b["verdict"][:nh])
+        # tokens for every Huffman string; meaningful where name_sel is set
+        lookup_tokens_dev(self.codec, b["dst"], ck, b["tokens"][:nh])
+        b.update({"nspans": ns, "nhuff": nh, "name_sel": ((hs[:, 1] >> 32) & SPAN_NAME) != 0})
         return b
 
     def decode_blocks(self, src, blocks):

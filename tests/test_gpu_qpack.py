@@ -167,8 +167,12 @@ def _gpu_scan(dec, src, blocks):
     d_ls = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
     d_ss = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
     d_st = torch.full((max(n, 1),), 7, dtype=torch.int32, device="cuda")
-    qpack.scan_blocks_dev(dec.codec, d_src, d_blk, d_lines, d_spans, d_ls, d_ss, d_st)
+    d_h = torch.zeros((cap, 2), dtype=torch.int64, device="cuda")
+    tot = qpack.scan_blocks_dev(dec.codec, d_src, d_blk, d_lines, d_spans, d_ls, d_ss, d_st, d_h)
     torch.cuda.synchronize()
+    sp = d_spans.cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1)[:tot[1]]
+    hsp = d_h.cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1)[:tot[2]]
+    assert hsp.tobytes() == sp[(sp["flags"] & qpack.SPAN_HUFFMAN) != 0].tobytes()
     ls = d_ls.cpu().numpy().view(np.uint32)
     ss = d_ss.cpu().numpy().view(np.uint32)
     lines = d_lines.cpu().numpy().view(qpack.FIELD_LINE_DTYPE)[:ls[n]]
@@ -212,13 +216,16 @@ def test_device_pipeline_matches_staged_path(dec):
     torch.cuda.synchronize()
     assert (d["status"][:blocks.size].cpu().numpy() == res["status"]).all()
     assert d["nspans"] == res["spans"].size
-    out = d["out"].cpu().numpy()
+    nh = d["nhuff"]
+    assert nh == res["huffman"].sum()
+    out = d["out"][:nh].cpu().numpy()
     dst = d["dst"].cpu().numpy()
     ho = res["out"]
     for k in range(ho.size):
         a = bytes(res["dst"][ho["off"][k]:ho["off"][k] + ho["len"][k]])
         b = bytes(dst[out[k, 0]:out[k, 0] + (out[k, 1] & 0xFFFFFFFF)])
         assert a == b
-    assert (d["verdict"].cpu().numpy() == res["verdict"][res["huffman"]]).all()
-    names = [bytes(dst[o:o + (l & 0xFFFFFFFF)]) for o, l in out[d["name_sel"].cpu().numpy()]]
-    assert (d["tokens"].cpu().numpy() == [qpack.lookup_token(x) for x in names]).all()
+    assert (d["verdict"][:nh].cpu().numpy() == res["verdict"][res["huffman"]]).all()
+    sel = d["name_sel"].cpu().numpy()
+    names = [bytes(dst[o:o + (l & 0xFFFFFFFF)]) for o, l in out[sel]]
+    assert (d["tokens"][:nh].cpu().numpy()[sel] == [qpack.lookup_token(x) for x in names]).all()
