@@ -358,7 +358,6 @@ class FieldSectionDecoder:
                  "line_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
                  "span_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
                  "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
-                 "dst": torch.empty(cap * 8 // 5 + 79 * cap + 64, dtype=torch.uint8, device=dev),
                  "out": torch.empty((cap, 2), dtype=torch.int64, device=dev),
                  "ck": torch.empty((cap, 2), dtype=torch.int64, device=dev),
                  "verdict": torch.empty(cap, dtype=torch.int8, device=dev),
@@ -366,6 +365,9 @@ class FieldSectionDecoder:
         _, ns, nh = scan_blocks_dev(self.codec, src, blocks, b["lines"], b["spans"],
                                     b["line_start"][:n + 1], b["span_start"][:n + 1],
                                     b["status"][:n], b["hspans"])
+        need = cap * 8 // 5 + 79 * nh + 64  # >= the slots of the nh strings
+        if "dst" not in b or b["dst"].numel() < need:
+            b["dst"] = torch.empty(need, dtype=torch.uint8, device=dev)
         hs, out, ck = b["hspans"][:nh], b["out"][:nh], b["ck"][:nh]
         if nh:
             self.codec.decode_dev(src, hs, b["dst"], out)
