@@ -252,7 +252,8 @@ def main():
     if not args.no_configs:
         from nghttp3_amd import qpack as qp
         nb_all = 65536
-        b_lo, b_hi = rank * nb_all // world, (rank + 1) * nb_all // world
+        from nghttp3_amd import shard as _shard
+        b_lo, b_hi = _shard.block_range(rank, world, nb_all)
         q_src, q_blocks, q_plain, q_strs, q_lines, q_ls = qp.synth_field_sections(0x5EED0004, nb_all)
         my = q_blocks[b_lo:b_hi].copy()
         base = int(my["off"][0])

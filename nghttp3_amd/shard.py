@@ -74,3 +74,10 @@ def output_offsets(local_bytes: int, dist=None, device=None) -> int:
     parts = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
     return int(sum(int(p.item()) for p in parts[:rank]))
+
+
+def block_range(rank: int, world: int, nblocks: int):
+    """Config 4: rank's contiguous range of header blocks, [lo, hi).  Blocks
+    at dynamic table 0 are independent, so ranks share nothing but the
+    report (strong scaling over a fixed block count)."""
+    return rank * nblocks // world, (rank + 1) * nblocks // world

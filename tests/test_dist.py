@@ -77,3 +77,44 @@ def test_split_by_bytes_edges():
     r = shard.split_by_bytes([1] * 10, 3)
     assert r[0][0] == 0 and r[-1][1] == 10
     assert sum(e - b for b, e in r) == 10
+
+
+def block_worker(rank, world, port, q):
+    """Config 4 at world size 2: each rank frames its block range alone."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nghttp3_amd import qpack
+        src, blocks, *_ = qpack.synth_field_sections(0x5EED0004, 3001)
+        lo, hi = shard.block_range(rank, world, blocks.size)
+        lines, spans, ls, ss, st = qpack.scan_blocks(src, blocks[lo:hi])
+        local = {"blocks": hi - lo, "lines": int(lines.size), "spans": int(spans.size),
+                 "errors": int((st != 0).sum()), "time_max": float(rank + 1)}
+        rep = shard.reduce_report(local, dist)
+        q.put((rank, lo, hi, rep, spans.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_blocks_gloo():
+    from nghttp3_amd import qpack
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=block_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    src, blocks, *_ = qpack.synth_field_sections(0x5EED0004, 3001)
+    lines, spans, ls, ss, st = qpack.scan_blocks(src, blocks)
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == blocks.size
+    assert b"".join(r[4] for r in res) == spans.tobytes()
+    rep = res[0][3]
+    assert rep == res[1][3]
+    assert rep["blocks"] == blocks.size and rep["lines"] == lines.size
+    assert rep["spans"] == spans.size and rep["errors"] == 0 and rep["time_max"] == world
