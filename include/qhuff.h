@@ -209,9 +209,11 @@ QH_EXPORT int qh_ctx_kernel_times(qh_ctx *ctx, const char **names,
 QH_EXPORT int qh_synth_spans(qh_ctx *ctx, uint64_t seed, size_t n, uint32_t lo,
                              uint32_t hi, int dist, double zipf_s,
                              qh_span_in *in_dev, uint64_t *total_dev);
-QH_EXPORT int qh_synth_fill(qh_ctx *ctx, uint64_t seed, uint8_t *dst_dev,
-                            uint64_t nbytes, const uint8_t *alphabet,
-                            uint32_t alphabet_len);
+/* dst_dev[j] = byte first + j of that packed buffer (a rank generates its
+ * own shard of a batch). */
+QH_EXPORT int qh_synth_fill(qh_ctx *ctx, uint64_t seed, uint64_t first,
+                            uint8_t *dst_dev, uint64_t nbytes,
+                            const uint8_t *alphabet, uint32_t alphabet_len);
 
 /* ---- QPACK field-line framing ---------
  * Host C (nghttp3_amd/csrc/qh_qpack.c).  The scanners turn whole encoded
@@ -267,11 +269,18 @@ typedef struct qh_section_prefix {
 
 /* Scans one complete field section (fin = 1).  Returns 0, or the error
  * nghttp3_qpack_decoder_read_request would return for it:
- * QH_ERR_QPACK_DECOMPRESSION_FAILED (integer overflow, or a representation
- * cut by the end of the section, :3780-3784), QH_ERR_QPACK_HEADER_TOO_LARGE
+ * QH_ERR_QPACK_DECOMPRESSION_FAILED (integer overflow, a representation cut
+ * by the end of the section, :3780-3784, or an index no table state can
+ * make valid: a static index >= 99, :3992 -> :2796-2797; with Required
+ * Insert Count 0 a negative Delta Base, :3414-3418, or any dynamic
+ * reference, :3985-3987, :4009-4011), QH_ERR_QPACK_HEADER_TOO_LARGE
  * (name > 256 / value > 65536 bytes, Huffman ones by their len*8/5
  * estimate, :3575-3588, :3661-3674), or QH_ERR_NOMEM when lines_cap /
- * spans_cap is too small.  Span offsets are src_off + position in src. */
+ * spans_cap is too small.  On an error *nlines is 0 and *nspans counts the
+ * strings read before it (the reference decodes those first, so a Huffman
+ * failure among them takes precedence: -401).  Span offsets are src_off +
+ * position in src.  Indices are not resolved: a section with a non-zero
+ * Required Insert Count frames fine whatever the dynamic table holds. */
 QH_EXPORT int qh_qpack_scan_field_section(
     const uint8_t *src, size_t srclen, uint64_t src_off,
     qh_section_prefix *prefix, qh_field_line *lines, size_t lines_cap,
@@ -280,8 +289,9 @@ QH_EXPORT int qh_qpack_scan_field_section(
 /* Batch of field sections: block i is src[blocks[i].off, +len).  Lines and
  * spans of block i are [line_start[i], line_start[i+1]) and likewise for
  * spans (both arrays hold nblocks + 1 entries); status[i] is block i's
- * verdict (a failed block contributes no lines or spans).  Returns 0, or
- * QH_ERR_NOMEM when the caps are exceeded. */
+ * framing verdict (a failed block contributes no lines, and the spans it
+ * read before the error).  Returns 0, or QH_ERR_NOMEM when the caps are
+ * exceeded. */
 QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
                                    const qh_span_in *blocks, size_t nblocks,
                                    qh_field_line *lines, size_t lines_cap,
@@ -305,9 +315,63 @@ QH_EXPORT int qh_scan_blocks_batch(qh_ctx *ctx, const uint8_t *src,
                                    size_t huff_cap, uint64_t *totals,
                                    int where);
 
+/* ---- Whole field sections in one call (decoder side of config 4) -------
+ * Replaces the request-stream decode loop of nghttp3_qpack_decoder_read_request
+ * (lib/nghttp3_qpack.c:3347-3805) for a batch of complete, independent field
+ * sections (fin = 1 each): framing (the parser above), every Huffman string
+ * decoded by the batch kernels (qpack_read_huffman_string, :2737-2763), a
+ * Huffman failure turned into the block's DECOMPRESSION_FAILED (:3604-3609,
+ * :3693-3698), then per string the field name / value check of
+ * nghttp3_check_header_name / _value (http.c:691-709, :798-838) and, for
+ * names, the token of qpack_lookup_token (qpack.c:342; the reference
+ * computes it on emit, :4130).
+ *
+ * Outputs are caller-allocated (HBM for QH_WHERE_DEVICE, host memory for
+ * QH_WHERE_HOST, where the call stages through the device and blocks):
+ *   lines / spans / line_start / span_start / status -- as qh_qpack_scan_blocks
+ *     (lines_cap, spans_cap >= total block bytes + 1 always suffice);
+ *   strs[k]    -- string k: a Huffman string decoded into dst (off, len in
+ *                 dst, status 0 or QH_ERR_QPACK_FATAL); a raw string is not
+ *                 copied (off, len in src, status 0);
+ *   verdict[k] -- 1 valid / 0 not (0 for a failed Huffman string); optional;
+ *   token[k]   -- nghttp3_qpack_token of a name, -1 otherwise; optional;
+ *   dst        -- decoded Huffman strings, qh_decode_batch's slot layout in
+ *                 Huffman-string order; dst_cap >= the `dst_need` total.
+ * status[b] is 0 or the reference's error for the block: its first framing
+ * error, unless a Huffman string before it fails (-401).
+ * Totals (nlines, nspans, nhuff, dst_need) are filled in on return, also on
+ * QH_ERR_NOMEM (caps or dst_cap too small: nothing was decoded; resize and
+ * call again).  opts: QH_SECTIONS_DTABLE0 decodes as a decoder whose
+ * dynamic table capacity is 0 (qpack_decode -s 0): any Required Insert
+ * Count but 0 fails the block (reconstruct_ricnt, :3915-3950). */
+#define QH_SECTIONS_DTABLE0 0x1u
+
+typedef struct qh_sections {
+  qh_field_line *lines;
+  size_t lines_cap;
+  qh_span_in *spans;
+  size_t spans_cap;
+  qh_span_out *strs;
+  int8_t *verdict;
+  int32_t *token;
+  uint32_t *line_start; /* nblocks + 1 */
+  uint32_t *span_start; /* nblocks + 1 */
+  int32_t *status;      /* nblocks     */
+  uint8_t *dst;
+  uint64_t dst_cap;
+  /* filled in by the call */
+  uint64_t nlines, nspans, nhuff, dst_need;
+} qh_sections;
+
+QH_EXPORT int qh_decode_sections_batch(qh_ctx *ctx, const uint8_t *src,
+                                       const qh_span_in *blocks,
+                                       size_t nblocks, uint32_t opts,
+                                       qh_sections *out, int where);
+
 /* Scans encoder-stream bytes.  Returns the number of bytes of complete
  * instructions (a trailing partial instruction is left for the next call,
- * like the streaming decoder), QH_ERR_QPACK_ENCODER_STREAM_ERROR,
+ * like the streaming decoder), QH_ERR_QPACK_ENCODER_STREAM_ERROR (also for
+ * a static name reference >= 99, qpack.c:2916 -> :3965-3966),
  * QH_ERR_QPACK_HEADER_TOO_LARGE or QH_ERR_NOMEM. */
 QH_EXPORT nghttp3_ssize qh_qpack_scan_encoder_stream(
     const uint8_t *src, size_t srclen, uint64_t src_off, qh_field_line *insts,
@@ -365,10 +429,10 @@ QH_EXPORT int nghttp3_check_header_value(const uint8_t *value, size_t len);
 
 /* Batch form on the GPU: verdict[i] = nghttp3_check_header_name of string i
  * if in[i].flags has QH_SPAN_NAME, else nghttp3_check_header_value (1 valid,
- * 0 not).  Meant to run on the decode destination right after
- * qh_decode_batch (its 64-byte slots satisfy the padding rule): device
- * strings are read in aligned 16-byte chunks, so a device buffer must extend
- * to the next multiple of 16 past each string.  Host batches are staged. */
+ * 0 not), e.g. over the decode destination right after qh_decode_batch.
+ * Device strings are read in aligned 16-byte chunks that each hold a byte
+ * of the string (so no load leaves the string's pages; no padding is
+ * needed).  Host batches are staged. */
 QH_EXPORT int qh_check_fields_batch(qh_ctx *ctx, const uint8_t *src,
                                     const qh_span_in *in, size_t n,
                                     int8_t *verdict, int where);

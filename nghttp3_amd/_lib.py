@@ -92,6 +92,7 @@ EXPORTED_FUNCTIONS = (
     "qh_qpack_scan_field_section",
     "qh_qpack_scan_blocks",
     "qh_scan_blocks_batch",
+    "qh_decode_sections_batch",
     "qh_qpack_scan_encoder_stream",
     "qh_qpack_put_varint_len",
     "qh_qpack_put_varint",
@@ -171,7 +172,7 @@ def load():
     lib.qh_ctx_kernel_times.restype = i32
     lib.qh_synth_spans.argtypes = [vp, u64, sz, u32, u32, i32, c.c_double, vp, vp]
     lib.qh_synth_spans.restype = i32
-    lib.qh_synth_fill.argtypes = [vp, u64, vp, u64, vp, u32]
+    lib.qh_synth_fill.argtypes = [vp, u64, u64, vp, u64, vp, u32]
     lib.qh_synth_fill.restype = i32
     lib.qh_version.argtypes = []
     lib.qh_version.restype = c.c_char_p

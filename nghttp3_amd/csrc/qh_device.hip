@@ -48,4 +48,5 @@
 #include "qh_api.inc"    // host API (include/qhuff.h)
 #include "qh_validate.inc"  // field name / value validation batch, header-name tokens
 #include "qh_frame.inc"     // QPACK field-section framing on the device
+#include "qh_sections.inc"  // whole field sections: frame -> decode -> fold / check / tokens
 

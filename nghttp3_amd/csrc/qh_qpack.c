@@ -35,7 +35,7 @@ QH_EXPORT int qh_qpack_scan_field_section(
   const uint8_t *src, size_t srclen, uint64_t src_off,
   qh_section_prefix *prefix, qh_field_line *lines, size_t lines_cap,
   size_t *nlines, qh_span_in *spans, size_t spans_cap, size_t *nspans) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0};
+  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
   int rv;
 
   if ((src == NULL && srclen) || nlines == NULL || nspans == NULL ||
@@ -43,7 +43,7 @@ QH_EXPORT int qh_qpack_scan_field_section(
     return QH_ERR_INVALID_ARGUMENT;
   }
   rv = scan_section(&o, src, srclen, src_off, prefix);
-  *nlines = o.nlines;
+  *nlines = rv ? 0 : o.nlines; /* on error: no lines, the strings read so far */
   *nspans = o.nspans;
   return rv;
 }
@@ -54,7 +54,7 @@ QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
                                    qh_span_in *spans, size_t spans_cap,
                                    uint32_t *line_start, uint32_t *span_start,
                                    int32_t *status) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0};
+  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
   size_t i;
 
   if ((src == NULL && nblocks) || (blocks == NULL && nblocks) ||
@@ -76,9 +76,9 @@ QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
       return QH_ERR_NOMEM;
     }
     status[i] = rv;
-    if (rv != 0) { /* a bad section contributes nothing */
+    if (rv != 0) { /* a bad section keeps the strings read before the error,
+                      and no lines */
       o.nlines = l0;
-      o.nspans = s0;
     }
   }
   line_start[nblocks] = (uint32_t)o.nlines;
@@ -90,7 +90,7 @@ QH_EXPORT nghttp3_ssize qh_qpack_scan_encoder_stream(
   const uint8_t *src, size_t srclen, uint64_t src_off, qh_field_line *insts,
   size_t insts_cap, size_t *ninsts, qh_span_in *spans, size_t spans_cap,
   size_t *nspans) {
-  scan_out o = {insts, insts_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0};
+  scan_out o = {insts, insts_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
   const uint8_t *p = src, *end = src + srclen, *done = src;
   const int bad = QH_ERR_QPACK_ENCODER_STREAM_ERROR;
   const int big = QH_ERR_QPACK_HEADER_TOO_LARGE; /* qpack.c:2962-2972 */
@@ -114,6 +114,12 @@ QH_EXPORT nghttp3_ssize qh_qpack_scan_encoder_stream(
         break;
       }
       rv = read_varint(&l->index, &p, end, 6);
+      /* rel2abs -> validate_index (qpack.c:3952-3969, :2796-2797): a
+       * static name reference must be < 99, whatever the table holds */
+      if (rv > 0 && !(l->flags & QH_FL_DYNAMIC) &&
+          l->index >= QH_QPACK_STATIC_ENTRIES) {
+        rv = bad;
+      }
       if (rv > 0) {
         rv = read_string(&o, &l->value, src, src_off, &p, end, 7,
                          QH_QPACK_MAX_VALUELEN, 0, big, bad);

@@ -15,6 +15,7 @@
 #define QH_QPACK_INT_MAX ((1ull << 62) - 1) /* nghttp3_qpack.h:43 */
 #define QH_QPACK_MAX_NAMELEN 256            /* nghttp3_qpack.h:47 */
 #define QH_QPACK_MAX_VALUELEN 65536         /* nghttp3_qpack.h:50 */
+#define QH_QPACK_STATIC_ENTRIES 99          /* stable[], qpack.c:52-189 */
 
 /* Reads an N-bit-prefix integer starting at *pp (the first byte's prefix
  * bits).  Returns 1 when complete, 0 when the input ends first, or
@@ -64,7 +65,9 @@ typedef struct scan_out {
   qh_span_in *spans;
   size_t spans_cap, nspans;
   qh_field_line scratch;
-  size_t nhuff; /* Huffman-coded strings seen */
+  size_t nhuff;    /* Huffman-coded strings seen */
+  uint64_t hslots; /* their batch-decode slot bytes (include/qhuff.h) */
+  uint32_t opts; /* QH_SECTIONS_DTABLE0: the decoder's table capacity is 0 */
 } scan_out;
 
 /* One string literal: H bit at bit `prefix` of the first byte, then the
@@ -112,6 +115,8 @@ QH_HD static inline int read_string(scan_out *o, int32_t *span_idx, const uint8_
   }
   *span_idx = (int32_t)o->nspans++;
   o->nhuff += h ? 1 : 0;
+  /* the slot qh_decode_batch gives it: len * 8 / 5 + 16, rounded up to 64 */
+  o->hslots += h ? ((len * 8 / 5 + 16 + 63) & ~(uint64_t)63) : 0;
   *pp = p + len;
   return 1;
 }
@@ -148,6 +153,12 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
   if (rv <= 0) {
     return bad;
   }
+  /* nghttp3_qpack_decoder_reconstruct_ricnt (qpack.c:3915-3950): with a
+   * hard table capacity of 0 there are no entries (full = 0), so any
+   * encoded count but 0 fails. */
+  if ((o->opts & QH_SECTIONS_DTABLE0) && pf.ricnt != 0) {
+    return bad;
+  }
   if (p == end) {
     return bad;
   }
@@ -155,6 +166,12 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
   pf.reserved = 0;
   rv = read_varint(&pf.delta_base, &p, end, 7);
   if (rv <= 0) {
+    return bad;
+  }
+  /* qpack.c:3414-3418: a negative Delta Base needs ricnt > delta_base; an
+   * encoded count of 0 is a reconstructed count of 0 (:3919-3921), whatever
+   * the table holds. */
+  if (pf.sign && pf.ricnt == 0) {
     return bad;
   }
   if (prefix) {
@@ -201,6 +218,17 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
       rv = read_varint(&l->index, &p, end, iprefix);
       if (rv <= 0) {
         return bad; /* overflow, or unfinished at fin (:3780-3784) */
+      }
+      /* brel2abs / pbrel2abs (qpack.c:3971-4017), the checks that need no
+       * table state: a static index must be < 99 (validate_index,
+       * :2796-2797); with Required Insert Count 0 every dynamic reference
+       * has absidx >= ricnt = 0 (:3985-3987, :4009-4011). */
+      if (flags & QH_FL_DYNAMIC) {
+        if (pf.ricnt == 0) {
+          return bad;
+        }
+      } else if (l->index >= QH_QPACK_STATIC_ENTRIES) {
+        return bad;
       }
     } else {
       rv = read_string(o, &l->name, src, src_off, &p, end, 3,

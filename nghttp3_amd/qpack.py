@@ -44,6 +44,21 @@ class qh_section_prefix(ctypes.Structure):
                 ("sign", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+SECTIONS_DTABLE0 = 0x1
+
+
+class qh_sections(ctypes.Structure):
+    """include/qhuff.h qh_sections (outputs of qh_decode_sections_batch)."""
+    _fields_ = [("lines", ctypes.c_void_p), ("lines_cap", ctypes.c_size_t),
+                ("spans", ctypes.c_void_p), ("spans_cap", ctypes.c_size_t),
+                ("strs", ctypes.c_void_p), ("verdict", ctypes.c_void_p),
+                ("token", ctypes.c_void_p), ("line_start", ctypes.c_void_p),
+                ("span_start", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_uint64),
+                ("nlines", ctypes.c_uint64), ("nspans", ctypes.c_uint64),
+                ("nhuff", ctypes.c_uint64), ("dst_need", ctypes.c_uint64)]
+
+
 _L = None
 
 
@@ -88,6 +103,9 @@ def _load():
         lib.qh_qpack_lookup_token.restype = c.c_int32
         lib.qh_lookup_tokens_batch.argtypes = [vp, vp, vp, sz, vp, i32]
         lib.qh_lookup_tokens_batch.restype = i32
+        lib.qh_decode_sections_batch.argtypes = [vp, vp, vp, sz, c.c_uint32, c.POINTER(qh_sections),
+                                                 i32]
+        lib.qh_decode_sections_batch.restype = i32
         _L = lib
     return _L
 
@@ -106,7 +124,8 @@ def _vp(a):
 
 def scan_field_section(buf, base_off: int = 0):
     """One complete field section -> (status, (ricnt, sign, delta_base) or
-    None, lines FIELD_LINE_DTYPE, spans SPAN_IN_DTYPE)."""
+    None, lines FIELD_LINE_DTYPE, spans SPAN_IN_DTYPE).  On an error there
+    are no lines and the spans are the strings read before it."""
     lib = _load()
     src = _u8(buf)
     cap = src.size + 1  # every line and string takes at least one byte
@@ -117,7 +136,7 @@ def scan_field_section(buf, base_off: int = 0):
     rv = lib.qh_qpack_scan_field_section(_vp(src), src.size, base_off, ctypes.byref(pf), _vp(lines),
                                          cap, ctypes.byref(nl), _vp(spans), cap, ctypes.byref(ns))
     if rv != 0:
-        return rv, None, lines[:0], spans[:0]
+        return rv, None, lines[:0], spans[:ns.value]
     return 0, (pf.ricnt, pf.sign, pf.delta_base), lines[:nl.value], spans[:ns.value]
 
 
@@ -326,85 +345,96 @@ def lookup_tokens_dev(codec: HuffmanBatchCodec, src, spans, token):
 
 
 class FieldSectionDecoder:
-    """Whole header blocks -> every string of every block, decoded.
+    """Whole header blocks -> every string of every block, decoded, checked
+    and (names) tokenised, through one qh_decode_sections_batch call: GPU
+    framing, the batch Huffman decoder, a failed Huffman string failing its
+    block with -401 as read_request does (qpack.c:3604-3609, :3693-3698),
+    the field name / value check and token lookup of every string.
 
-    The framing scan runs on the host (C); all Huffman strings of the batch
-    then go to the GPU in one qh_decode_batch.  Returns per string the
-    decoded bytes' (off, len, status) in one output buffer; raw (non-H)
-    strings are reported as spans into the input."""
+    ``decode_blocks`` takes host arrays (the library stages them);
+    ``decode_blocks_dev`` takes tensors already in HBM.  ``dtable0`` decodes
+    as a decoder whose dynamic table capacity is 0 (config 4)."""
 
-    def __init__(self, device: int = 0, codec: HuffmanBatchCodec | None = None):
+    def __init__(self, device: int = 0, codec: HuffmanBatchCodec | None = None,
+                 dtable0: bool = False):
         self.codec = codec or HuffmanBatchCodec(device)
+        self.opts = SECTIONS_DTABLE0 if dtable0 else 0
 
     def decode_blocks_dev(self, src, blocks, bufs=None):
-        """Device-resident pipeline: header blocks already in HBM (src uint8,
-        blocks int64 [n,2]) -> GPU framing, decode of every Huffman string,
-        validation of every Huffman-coded name / value and tokens of those
-        names, with no host round trip of string data (one small sync in
-        the framing call).  Returns a dict of torch tensors; `bufs` (the
-        dict of a previous call) reuses its allocations."""
+        """src uint8 and blocks int64 [n,2] (SPAN_IN layout) torch tensors in
+        HBM.  Returns a dict of torch tensors (lines, spans, strs, verdict,
+        tokens, line_start, span_start, status, dst) plus the totals
+        (nlines, nspans, nhuff, dst_need); `bufs` (a previous result)
+        reuses its allocations.  Asynchronous after the framing sync."""
         import torch
         dev = src.device
         n = blocks.shape[0]
         b = bufs or {}
-        cap = int(src.numel()) + 1
+        cap = int(src.numel()) + 1  # every line and string takes >= 1 byte
         if b.get("cap", -1) < cap or b.get("n", -1) < n:
-            # every line and string takes at least one byte of the blocks;
-            # a decode slot is at most len * 8 / 5 + 16 rounded up to 64
             b = {"cap": cap, "n": n,
                  "lines": torch.empty(cap * FIELD_LINE_DTYPE.itemsize, dtype=torch.uint8, device=dev),
                  "spans": torch.empty((cap, 2), dtype=torch.int64, device=dev),
-                 "hspans": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "strs": torch.empty((cap, 2), dtype=torch.int64, device=dev),
+                 "verdict": torch.empty(cap, dtype=torch.int8, device=dev),
+                 "tokens": torch.empty(cap, dtype=torch.int32, device=dev),
                  "line_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
                  "span_start": torch.empty(n + 1, dtype=torch.int32, device=dev),
                  "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
-                 "out": torch.empty((cap, 2), dtype=torch.int64, device=dev),
-                 "ck": torch.empty((cap, 2), dtype=torch.int64, device=dev),
-                 "verdict": torch.empty(cap, dtype=torch.int8, device=dev),
-                 "tokens": torch.empty(cap, dtype=torch.int32, device=dev)}
-        _, ns, nh = scan_blocks_dev(self.codec, src, blocks, b["lines"], b["spans"],
-                                    b["line_start"][:n + 1], b["span_start"][:n + 1],
-                                    b["status"][:n], b["hspans"])
-        need = cap * 8 // 5 + 79 * nh + 64  # >= the slots of the nh strings
-        if "dst" not in b or b["dst"].numel() < need:
-            b["dst"] = torch.empty(need, dtype=torch.uint8, device=dev)
-        hs, out, ck = b["hspans"][:nh], b["out"][:nh], b["ck"][:nh]
-        if nh:
-            self.codec.decode_dev(src, hs, b["dst"], out)
-        # check / token spans: decoded (off, len) with the scanned flags
-        ck[:, 0] = out[:, 0]
-        ck[:, 1] = (out[:, 1] & 0xFFFFFFFF) | ((hs[:, 1] >> 32) << 32)
-        check_fields_dev(self.codec, b["dst"], ck, b["verdict"][:nh])
-        # tokens for every Huffman string; meaningful where name_sel is set
-        lookup_tokens_dev(self.codec, b["dst"], ck, b["tokens"][:nh])
-        b.update({"nspans": ns, "nhuff": nh, "name_sel": ((hs[:, 1] >> 32) & SPAN_NAME) != 0})
+                 "dst": torch.empty(64, dtype=torch.uint8, device=dev)}
+        lib = _load()
+        p = lambda t: t.data_ptr()
+        for _ in range(2):  # a second try only when dst was too small
+            st = qh_sections(p(b["lines"]), cap, p(b["spans"]), cap, p(b["strs"]), p(b["verdict"]),
+                             p(b["tokens"]), p(b["line_start"]), p(b["span_start"]), p(b["status"]),
+                             p(b["dst"]), b["dst"].numel(), 0, 0, 0, 0)
+            rv = lib.qh_decode_sections_batch(self.codec._ctx, ctypes.c_void_p(src.data_ptr()),
+                                              ctypes.c_void_p(blocks.data_ptr()), n, self.opts,
+                                              ctypes.byref(st), _lib.QH_WHERE_DEVICE)
+            if rv == _lib.QH_ERR_NOMEM and st.dst_need > b["dst"].numel():
+                b["dst"] = torch.empty(int(st.dst_need), dtype=torch.uint8, device=dev)
+                continue
+            _lib.check(rv, "qh_decode_sections_batch")
+            break
+        b.update({"nlines": st.nlines, "nspans": st.nspans, "nhuff": st.nhuff,
+                  "dst_need": st.dst_need})
         return b
 
     def decode_blocks(self, src, blocks):
+        """Host arrays in and out: -> dict with lines, spans, strs
+        (SPAN_OUT_DTYPE: Huffman strings in dst, raw strings in src),
+        huffman (bool per span), verdict, tokens, line_start, span_start,
+        status, dst."""
+        lib = _load()
         src = _u8(src)
-        lines, spans, ls, ss, status = scan_blocks(src, blocks)
-        huff = (spans["flags"] & SPAN_HUFFMAN) != 0
-        hspans = np.ascontiguousarray(spans[huff])
-        if hspans.size:
-            dst, out = self.codec.decode_host(src, hspans)
-        else:
-            dst, out = np.zeros(1, np.uint8), np.zeros(0, SPAN_OUT_DTYPE)
-        # a Huffman error fails its whole block (qpack.c:3608-3609 -> -401)
-        bad = out["status"] != 0
-        if bad.any():
-            owner = np.searchsorted(ss, np.nonzero(huff)[0][bad], side="right") - 1
-            status[np.unique(owner)] = QH_ERR_QPACK_DECOMPRESSION_FAILED
-        # field name / value validation of every string (qpack.c hands the
-        # decoded nv to http.c:383-528, which checks it with
-        # nghttp3_check_header_name / _value): Huffman strings in the
-        # decode destination, raw ones in place
-        verdict = np.zeros(spans.size, dtype=np.int8)
-        if hspans.size:
-            dsp = np.zeros(hspans.size, dtype=SPAN_IN_DTYPE)
-            dsp["off"], dsp["len"] = out["off"], out["len"]
-            dsp["flags"] = hspans["flags"]
-            verdict[huff] = check_fields_host(self.codec, dst, dsp)
-        if (~huff).any():
-            verdict[~huff] = check_fields_host(self.codec, src, np.ascontiguousarray(spans[~huff]))
-        return {"lines": lines, "spans": spans, "line_start": ls, "span_start": ss,
-                "status": status, "huffman": huff, "dst": dst, "out": out, "verdict": verdict}
+        if src.size == 0:
+            src = np.zeros(1, dtype=np.uint8)
+        blocks = np.ascontiguousarray(blocks, dtype=SPAN_IN_DTYPE)
+        n = blocks.size
+        cap = int(blocks["len"].sum(dtype=np.uint64)) + 1
+        lines = np.zeros(cap, dtype=FIELD_LINE_DTYPE)
+        spans = np.zeros(cap, dtype=SPAN_IN_DTYPE)
+        strs = np.zeros(cap, dtype=SPAN_OUT_DTYPE)
+        verdict = np.zeros(cap, dtype=np.int8)
+        tokens = np.zeros(cap, dtype=np.int32)
+        ls = np.zeros(n + 1, dtype=np.uint32)
+        ss = np.zeros(n + 1, dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        dst = np.zeros(64, dtype=np.uint8)
+        for _ in range(2):
+            st = qh_sections(lines.ctypes.data, cap, spans.ctypes.data, cap, strs.ctypes.data,
+                             verdict.ctypes.data, tokens.ctypes.data, ls.ctypes.data, ss.ctypes.data,
+                             status.ctypes.data, dst.ctypes.data, dst.size, 0, 0, 0, 0)
+            rv = lib.qh_decode_sections_batch(self.codec._ctx, _vp(src), _vp(blocks), n, self.opts,
+                                              ctypes.byref(st), _lib.QH_WHERE_HOST)
+            if rv == _lib.QH_ERR_NOMEM and st.dst_need > dst.size:
+                dst = np.zeros(int(st.dst_need), dtype=np.uint8)
+                continue
+            _lib.check(rv, "qh_decode_sections_batch")
+            break
+        ns = int(st.nspans)
+        spans = spans[:ns]
+        return {"lines": lines[:st.nlines], "spans": spans, "strs": strs[:ns],
+                "huffman": (spans["flags"] & SPAN_HUFFMAN) != 0, "verdict": verdict[:ns],
+                "tokens": tokens[:ns], "line_start": ls, "span_start": ss, "status": status[:n],
+                "dst": dst}

@@ -223,11 +223,29 @@ class HuffmanBatchCodec:
                                             self._ptr(spans), self._ptr(total)), "qh_synth_spans")
         self.sync()
         nbytes = int(total.item())
-        src = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        return self.synth_fill(seed, 0, nbytes, alphabet), spans, nbytes
+
+    def synth_fill(self, seed: int, first: int, nbytes: int, alphabet: bytes):
+        """Bytes [first, first + nbytes) of the packed synthetic stream of
+        `seed` (nghttp3_amd/synth.py fill) as a uint8 tensor on the device."""
+        torch = _torch()
+        src = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", self.device))
         a = np.frombuffer(bytes(alphabet), dtype=np.uint8)
-        _lib.check(self._lib.qh_synth_fill(self._ctx, seed, self._ptr(src), nbytes,
+        _lib.check(self._lib.qh_synth_fill(self._ctx, seed, first, self._ptr(src), nbytes,
                                            a.ctypes.data_as(ctypes.c_void_p), a.size), "qh_synth_fill")
-        return src, spans, nbytes
+        return src
+
+    def spans_to_device(self, lengths):
+        """Packed spans (off = exclusive prefix of `lengths`) as an int64
+        [n, 2] tensor on the device, and the total bytes."""
+        torch = _torch()
+        ln = np.ascontiguousarray(lengths, dtype=np.int64)
+        off = np.zeros(ln.size, dtype=np.int64)
+        if ln.size:
+            off[1:] = np.cumsum(ln)[:-1]
+        sp = np.stack([off, ln], axis=1) if ln.size else np.zeros((0, 2), dtype=np.int64)
+        return torch.from_numpy(np.ascontiguousarray(sp)).to(torch.device("cuda", self.device)), \
+            int(ln.sum())
 
     # -- host batches (library stages H2D / D2H) ----------------------------
     def decode_host(self, src, spans, dst=None, out=None):

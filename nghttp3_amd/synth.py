@@ -45,13 +45,28 @@ def lengths(seed: int, n: int, lo: int, hi: int) -> np.ndarray:
     return (np.uint64(lo) + r % np.uint64(hi - lo + 1)).astype(np.uint32)
 
 
-def fill(seed: int, nbytes: int, alphabet: bytes, chunk: int = 1 << 24) -> np.ndarray:
+def fill(seed: int, nbytes: int, alphabet: bytes, chunk: int = 1 << 24, first: int = 0) -> np.ndarray:
+    """Bytes [first, first + nbytes) of the packed stream (qh_synth_fill)."""
     a = np.frombuffer(bytes(alphabet), dtype=np.uint8)
     out = np.empty(nbytes, dtype=np.uint8)
     for s in range(0, nbytes, chunk):
         m = min(chunk, nbytes - s)
-        out[s:s + m] = a[(draws(seed ^ BYTE_STREAM, s, m) % np.uint64(a.size)).astype(np.int64)]
+        out[s:s + m] = a[(draws(seed ^ BYTE_STREAM, first + s, m) % np.uint64(a.size)).astype(np.int64)]
     return out
+
+
+def zipf_lengths(seed: int, n: int, lo: int, hi: int, s: float) -> np.ndarray:
+    """Config 5's lengths: P(len = k) proportional to k^-s over [lo, hi]
+    (s = 1.2 over 1..4096, mean ~209 B), by inverse
+    CDF of the 53-bit uniform draw(seed ^ LEN_STREAM, i) / 2^53 (float64,
+    sequential cumsum: the same on every host)."""
+    k = np.arange(lo, hi + 1, dtype=np.float64)
+    w = k ** -float(s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    u = (draws(seed ^ LEN_STREAM, 0, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    idx = np.searchsorted(cdf, u, side="right")
+    return (lo + np.minimum(idx, hi - lo)).astype(np.uint32)
 
 
 def batch(seed: int, n: int, lo: int, hi: int, alphabet: bytes):

@@ -145,12 +145,11 @@ def decode_batch(enc, off, ln):
 
 
 def bench_roundtrip(plain, off, ln, nthreads: int, reps: int):
-    """CPU baseline: (encode seconds, decode seconds, ok)."""
+    """CPU baseline: per-rep (encode seconds, decode seconds) lists and ok."""
     plain = np.ascontiguousarray(plain, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     ln = np.ascontiguousarray(ln, dtype=np.uint32)
-    e = ctypes.c_double()
-    d = ctypes.c_double()
-    rv = load().qho_bench_roundtrip(_p(plain), _p(off), _p(ln), ln.size, nthreads, reps,
-                                    ctypes.byref(e), ctypes.byref(d))
-    return e.value, d.value, rv == 0
+    e = (ctypes.c_double * max(reps, 1))()
+    d = (ctypes.c_double * max(reps, 1))()
+    rv = load().qho_bench_roundtrip(_p(plain), _p(off), _p(ln), ln.size, nthreads, reps, e, d)
+    return list(e)[:reps], list(d)[:reps], rv == 0

@@ -360,16 +360,15 @@ int qho_bench_roundtrip(const uint8_t *src, const uint64_t *off,
     sh[t].dec = (uint8_t *)malloc((size_t)maxlen * 30 / 8 * 8 / 5 + 16);
     sh[t].ok = 1;
   }
-  *enc_seconds = 0;
-  *dec_seconds = 0;
+  /* one entry per rep (CLOCK_MONOTONIC around each parallel phase) */
   for (r = 0; r < reps; ++r) {
     double t0 = now_s();
     run_phase(sh, nthreads, 0);
     double t1 = now_s();
     run_phase(sh, nthreads, 1);
     double t2 = now_s();
-    *enc_seconds += t1 - t0;
-    *dec_seconds += t2 - t1;
+    enc_seconds[r] = t1 - t0;
+    dec_seconds[r] = t2 - t1;
   }
   for (t = 0; t < nthreads; ++t) {
     ok &= sh[t].ok;

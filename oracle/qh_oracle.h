@@ -71,8 +71,9 @@ uint64_t qho_decode_batch(const uint8_t *src, const uint64_t *off,
 
 /* CPU baseline: round trip (encode_count + encode, then decode) of the n
  * strings on `nthreads` pthreads, each on a contiguous shard, repeated
- * `reps` times; CLOCK_MONOTONIC seconds for the encode and decode phases
- * (summed over reps). Returns 0 if every string round-tripped. */
+ * `reps` times; CLOCK_MONOTONIC seconds of the encode and decode phases of
+ * each rep in enc_seconds[r] / dec_seconds[r]. Returns 0 if every string
+ * round-tripped. */
 int qho_bench_roundtrip(const uint8_t *src, const uint64_t *off,
                         const uint32_t *len, size_t n, int nthreads, int reps,
                         double *enc_seconds, double *dec_seconds);

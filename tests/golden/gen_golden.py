@@ -230,6 +230,80 @@ def gen_digests(out):
               out, indent=1)
 
 
+# config 5 (16M Zipf strings over 8 GPUs): one rank's shard, as bench.py
+# cuts it; config 4: the whole 65,536-block corpus through the oracle
+C5 = dict(seed=synth.SEEDS[5], n_total=16 << 20, lo=1, hi=4096, s=1.2, world=8, rank=0,
+          alphabet="A")
+C4 = dict(seed=synth.SEEDS[4], nblocks=65536, dtable0=True)
+
+
+def gen_c5_shard():
+    from nghttp3_amd import shard
+    c = C5
+    ln = synth.zipf_lengths(c["seed"], c["n_total"], c["lo"], c["hi"], c["s"])
+    b, e = shard.split_by_bytes(ln, c["world"])[c["rank"]]
+    first = int(ln[:b].sum(dtype=np.uint64))
+    my = ln[b:e]
+    plain = synth.fill(c["seed"], int(my.sum(dtype=np.uint64)), alphabet(c["alphabet"]), first=first)
+    off = np.zeros(my.size, dtype=np.uint64)
+    off[1:] = np.cumsum(my.astype(np.uint64))[:-1]
+    enc, eoff, elen = oracle.encode_batch(plain, off, my)
+    r = dict(c, begin=int(b), end=int(e), first=first, plain_bytes=int(plain.size),
+             enc_bytes=int(enc.size), len_sha256=sha(my), plain_sha256=sha(plain),
+             enc_sha256=sha(enc), enc_len_sha256=sha(elen))
+    print("c5 shard", r["end"] - r["begin"], r["plain_bytes"], r["enc_bytes"])
+    return r
+
+
+def gen_c4_blocks():
+    """Block bytes from the product writer (pinned by the oracle writers in
+    tests/test_qpack.py); expected outputs from the oracle: every string
+    decoded in span order (oracle/qpack_frame.decode_field_section), its
+    verdict (oracle/http_check with the reference's tables) and a name's
+    token (the reference's enum)."""
+    from oracle import http_check, qpack_frame
+    from nghttp3_amd import qpack
+    chars = json.load(open(os.path.join(HERE, "http_chars.json")))
+    tokens = json.load(open(os.path.join(HERE, "tokens.json")))["tokens"]
+    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(C4["seed"], C4["nblocks"])
+    data = bytes(src)
+    out, verdict, token = [], [], []
+    nlines = 0
+    for b in range(blocks.size):
+        o, n = int(blocks["off"][b]), int(blocks["len"][b])
+        st, rl, rs, rstr = qpack_frame.decode_field_section(data[o:o + n], o, C4["dtable0"])
+        assert st == 0
+        nlines += len(rl)
+        for (so, sn, fl), v in zip(rs, rstr):
+            out.append(v)
+            if fl & qpack_frame.SPAN_NAME:
+                verdict.append(http_check.check_header_name(v, chars["VALID_HD_NAME_CHARS"]))
+                token.append(http_check.lookup_token(v, tokens))
+            else:
+                verdict.append(http_check.check_header_value(v, chars["VALID_HD_VALUE_CHARS"]))
+                token.append(-1)
+    strings = b"".join(out)
+    r = dict(C4, block_bytes=int(src.size), blocks_sha256=sha(src), field_lines=nlines,
+             strings=len(out), string_bytes=len(strings),
+             strings_sha256=hashlib.sha256(strings).hexdigest(),
+             verdict_sha256=sha(np.array(verdict, dtype=np.int8)),
+             token_sha256=sha(np.array(token, dtype=np.int32)))
+    print("c4", r["strings"], r["string_bytes"], r["field_lines"])
+    return r
+
+
+def update_digests(keys):
+    path = os.path.join(HERE, "digests.json")
+    d = json.load(open(path))
+    if "c5_r0of8" in keys:
+        d["configs"]["c5_r0of8"] = gen_c5_shard()
+    if "c4_blocks" in keys:
+        d["configs"]["c4_blocks"] = gen_c4_blocks()
+    d["source"] = "oracle outputs of nghttp3_amd.synth batches (gen_golden.py)"
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1)
+
+
 def main():
     with open(os.path.join(HERE, "tables.json.new"), "w") as f:
         gen_tables(f)
@@ -247,4 +321,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # e.g. gen_golden.py c5_r0of8 c4_blocks: just those digests
+        update_digests(sys.argv[1:])
+    else:
+        main()

@@ -254,6 +254,51 @@ def test_full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
+def test_config5_rank_shard_full_size(codec, digests):
+    """Config 5 at size: rank 0's shard of 16M Zipf strings split by bytes
+    over 8 GPUs (2.1M strings, 438 MB, lengths 1..4096), as bench.py cuts
+    it: the device generator from the global byte offset, encode digests vs
+    the oracle's, then the decode round trip (chunked compare)."""
+    from nghttp3_amd import shard
+    torch = torch_mod()
+    d = digests["c5_r0of8"]
+    ln_all = synth.zipf_lengths(d["seed"], d["n_total"], d["lo"], d["hi"], d["s"])
+    b, e = shard.split_by_bytes(ln_all, d["world"])[d["rank"]]
+    assert (b, e) == (d["begin"], d["end"])
+    my = ln_all[b:e]
+    assert sha(my) == d["len_sha256"]
+    first = int(ln_all[:b].sum(dtype=np.uint64))
+    spans, total = codec.spans_to_device(my)
+    src = codec.synth_fill(d["seed"], first, total, synth.ALPHABET_A)
+    assert total == d["plain_bytes"] and sha(src[:total].cpu().numpy()) == d["plain_sha256"]
+    n = e - b
+    enc = torch.zeros(int((my.astype(np.int64) * 30 + 7).sum() // 8) + 64, dtype=torch.uint8,
+                      device="cuda")
+    eout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    st = codec.stats()
+    assert st["n_errors"] == 0 and st["out_bytes"] == d["enc_bytes"]
+    elen = eout[:, 1] & 0xFFFFFFFF
+    assert sha(elen.cpu().numpy().astype(np.uint32)) == d["enc_len_sha256"]
+    assert sha(enc[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
+    cap = int(q.decode_slot_size(elen).sum().item())
+    dec = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    dout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(enc, eout, dec, dout)
+    st = codec.stats()
+    assert st["n_errors"] == 0 and st["out_bytes"] == total
+    ln = spans[:, 1]
+    assert bool(((dout[:, 1] & 0xFFFFFFFF) == ln).all()) and bool(((dout[:, 1] >> 32) == 0).all())
+    for i0 in range(0, n, 1 << 19):
+        i1 = min(n, i0 + (1 << 19))
+        l = ln[i0:i1]
+        t = int(l.sum().item())
+        pos = torch.arange(t, device="cuda", dtype=torch.int64) - \
+            torch.repeat_interleave(torch.cumsum(l, 0) - l, l)
+        assert bool((dec[torch.repeat_interleave(dout[i0:i1, 0], l) + pos] ==
+                     src[torch.repeat_interleave(spans[i0:i1, 0], l) + pos]).all())
+
+
 def test_encode_unordered_spans(codec, corpus):
     # spans in any order: same bytes, dense output in span order
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]

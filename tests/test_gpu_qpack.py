@@ -1,9 +1,10 @@
-"""GPU parity for QPACK field sections (SURVEY.md section 8(f) row 1):
-header blocks are framed on the host by nghttp3_amd/csrc/qh_qpack.c and
-every Huffman string of the batch is decoded by the HIP kernels through
-qh_decode_batch; the decoded strings must equal the oracle's (bit-exact),
-and a corrupted string must fail exactly its own block with -401, as
-nghttp3_qpack_decoder_read_request does (qpack.c:3604-3609, :3693-3698)."""
+"""GPU parity for QPACK field sections (SURVEY.md section 8(f) rows 1, 3, 4):
+qh_decode_sections_batch (GPU framing -> batch Huffman decode -> per-block
+fold, validation, tokens) against the oracle directly: per block the status
+of oracle/qpack_frame.decode_field_section (read_request restated, with a
+corrupted string failing exactly its own block with -401 as
+qpack.c:3604-3609, :3693-3698 do), per string the oracle's decoded bytes,
+oracle/http_check's verdict and the reference's token."""
 import os
 
 import numpy as np
@@ -24,19 +25,67 @@ def dec():
     return qpack.FieldSectionDecoder(0)
 
 
-def _check_strings(src, res):
-    spans, dst, out, huff = res["spans"], res["dst"], res["out"], res["huffman"]
-    hs = spans[huff]
-    for k in range(hs.size):
-        raw = bytes(src[hs["off"][k]:hs["off"][k] + hs["len"][k]])
-        st, want = oracle.decode_one(raw)
-        assert int(out["status"][k]) == st
-        if st == 0:
-            got = bytes(dst[out["off"][k]:out["off"][k] + out["len"][k]])
-            assert got == want
+@pytest.fixture(scope="module")
+def dec0(dec):
+    """Decoder at dynamic table capacity 0 (config 4), same context."""
+    return qpack.FieldSectionDecoder(codec=dec.codec, dtable0=True)
 
 
-def test_netbsd_blocks_decode_on_gpu(dec):
+@pytest.fixture(scope="module")
+def refdata():
+    from conftest import load_json
+    d = load_json("http_chars.json")
+    return d["VALID_HD_NAME_CHARS"], d["VALID_HD_VALUE_CHARS"], load_json("tokens.json")["tokens"]
+
+
+def _blocks_of(lens):
+    blocks = np.zeros(len(lens), dtype=SPAN_IN_DTYPE)
+    blocks["len"] = lens
+    if len(lens):
+        blocks["off"][1:] = np.cumsum(blocks["len"].astype(np.uint64))[:-1]
+    return blocks
+
+
+def _check_against_oracle(src, blocks, res, refdata, dtable0, strs_dst=None, src_bytes=None):
+    """Per block and per string, the C pipeline's result equals the oracle's
+    restatement of read_request (oracle/qpack_frame.decode_field_section:
+    framing + Huffman in stream order), oracle/http_check and the
+    reference's token table."""
+    from oracle import http_check
+    names, values, tokens = refdata
+    data = bytes(src) if src_bytes is None else src_bytes
+    dst = res["dst"] if strs_dst is None else strs_dst
+    ss, st = res["span_start"], res["status"]
+    nbad = 0
+    for b in range(blocks.size):
+        off, n = int(blocks["off"][b]), int(blocks["len"][b])
+        rst, rlines, rspans, rstrings = ref.decode_field_section(data[off:off + n], off, dtable0)
+        assert int(st[b]) == rst, (b, int(st[b]), rst)
+        nbad += rst != 0
+        k0, k1 = int(ss[b]), int(ss[b + 1])
+        assert k1 - k0 == len(rspans), b
+        got_spans = [(int(x["off"]), int(x["len"]), int(x["flags"])) for x in res["spans"][k0:k1]]
+        assert got_spans == rspans, b
+        for j, k in enumerate(range(k0, k1)):
+            o = res["strs"][k]
+            want = rstrings[j]
+            is_name = bool(rspans[j][2] & ref.SPAN_NAME)
+            if want is None:
+                assert int(o["status"]) == -108 and res["verdict"][k] == 0 and res["tokens"][k] == -1
+                continue
+            assert int(o["status"]) == 0
+            buf = dst if rspans[j][2] & ref.SPAN_HUFFMAN else src
+            got = bytes(buf[int(o["off"]):int(o["off"]) + int(o["len"])])
+            assert got == want, (b, j)
+            vw = http_check.check_header_name(want, names) if is_name else \
+                http_check.check_header_value(want, values)
+            assert res["verdict"][k] == vw, (b, j, want)
+            tw = http_check.lookup_token(want, tokens) if is_name else -1
+            assert res["tokens"][k] == tw, (b, j, want)
+    return nbad
+
+
+def test_netbsd_blocks_decode_on_gpu(dec, refdata):
     data = open(os.path.join(GOLDEN, "netbsd-hq.out.256.100.1"), "rb").read()
     recs = [r for r in ref.read_qif_out(data) if r[0] != 0]
     blocks = np.zeros(len(recs), dtype=SPAN_IN_DTYPE)
@@ -47,53 +96,134 @@ def test_netbsd_blocks_decode_on_gpu(dec):
     assert (res["status"] == 0).all()
     assert res["lines"].size == 199
     assert res["huffman"].sum() > 0
-    _check_strings(src, res)
+    assert _check_against_oracle(src, blocks, res, refdata, False) == 0
 
 
-def test_synthetic_sections_decode_on_gpu_with_corruption(dec):
-    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED0004, 4096)
-    src = src.copy()
-    ref_res = qpack.scan_blocks(src, blocks)
-    spans = ref_res[1]
-    hidx = np.nonzero(spans["flags"] & qpack.SPAN_HUFFMAN)[0]
-    # corrupt the last byte of a few Huffman strings into zero padding
-    rng = np.random.default_rng(7)
-    victims = rng.choice(hidx, 16, replace=False)
-    for v in victims:
-        src[spans["off"][v] + spans["len"][v] - 1] = 0x00
-    res = dec.decode_blocks(src, blocks)
-    _check_strings(src, res)
-    bad_blocks = set(np.searchsorted(ref_res[3], victims, side="right") - 1)
-    for b in range(blocks.size):
-        # a zeroed final byte is always invalid padding unless the string is
-        # still accepted (oracle decides); compare against the oracle's view
-        s0, s1 = ref_res[3][b], ref_res[3][b + 1]
-        want = 0
-        for k in range(s0, s1):
-            if spans["flags"][k] & qpack.SPAN_HUFFMAN:
-                raw = bytes(src[spans["off"][k]:spans["off"][k] + spans["len"][k]])
-                if oracle.decode_one(raw)[0] != 0:
-                    want = qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED
-        assert res["status"][b] == want, b
-    assert any(res["status"][b] != 0 for b in bad_blocks)
-    # clean blocks: every string equals the plaintext the writer was given
-    ok = res["status"] == 0
+def _corrupted_corpus(seed, nblocks):
+    """Synthetic config-4 blocks with every kind of bad input the reference
+    rejects, block by block: zero padding / EOS / over-long padding in
+    Huffman strings, a Huffman failure before a HEADER_TOO_LARGE, static
+    index >= 99, dynamic references and a negative Delta Base at Required
+    Insert Count 0, a non-zero Required Insert Count (capacity 0),
+    truncation, integer overflow."""
+    src, blocks, *_ = qpack.synth_field_sections(seed, nblocks)
+    secs = [bytes(src[int(o):int(o) + int(n)]) for o, n in zip(blocks["off"], blocks["len"])]
+    rng = np.random.default_rng(seed)
+    kinds = []
+    for b in rng.choice(nblocks, nblocks // 8, replace=False):
+        sec = bytearray(secs[b])
+        _, _, _, spans = ref.scan_field_section(bytes(sec))
+        hs = [sp for sp in spans if sp[2] & ref.SPAN_HUFFMAN]
+        kind = int(rng.integers(0, 10))
+        if kind == 0 and hs:       # last byte -> zero padding
+            o, n, _ = hs[int(rng.integers(len(hs)))]
+            sec[o + n - 1] = 0x00
+        elif kind == 1 and hs:     # EOS inside
+            o, n, _ = hs[int(rng.integers(len(hs)))]
+            if n >= 4:
+                sec[o:o + 4] = b"\xff\xff\xff\xff"
+        elif kind == 2 and hs:     # padding of 8+ ones
+            o, n, _ = hs[int(rng.integers(len(hs)))]
+            sec[o + n - 1] = 0xFF
+            if n >= 2:
+                sec[o + n - 2] = 0xFF
+        elif kind == 3:            # bad Huffman string, then a too-large value
+            sec += b"\x50\x81\x00\x50" + ref.put_varint(65537, 7) + b"a" * 65537
+        elif kind == 4:            # static index past the table
+            sec += ref.write_indexed(0xC0, int(rng.integers(99, 5000)), 6)
+        elif kind == 5:            # dynamic reference at ricnt 0
+            sec += ref.write_indexed(0x80, 0, 6)
+        elif kind == 6:            # negative Delta Base at ricnt 0
+            sec[1] |= 0x80
+        elif kind == 7:            # Required Insert Count 1 (capacity 0 rejects)
+            sec[0] = 0x01
+        elif kind == 8:            # truncated
+            sec = sec[:max(0, len(sec) - int(rng.integers(1, 4)))]
+        else:                      # integer overflow in a length
+            sec += b"\x2f" + b"\xff" * 12
+        secs[b] = bytes(sec)
+        kinds.append(kind)
+    data = b"".join(secs)
+    return np.frombuffer(data, dtype=np.uint8).copy(), _blocks_of([len(x) for x in secs]), kinds
+
+
+@pytest.mark.parametrize("dtable0", [False, True])
+def test_sections_pipeline_matches_oracle_on_corrupted_blocks(dec, dec0, refdata, dtable0):
+    """qh_decode_sections_batch, host and device forms, against the oracle
+    per block (status) and per string (bytes, verdict, token)."""
+    import torch
+    d = dec0 if dtable0 else dec
+    src, blocks, kinds = _corrupted_corpus(0x5EED0004 + dtable0, 3000)
+    res = d.decode_blocks(src, blocks)
+    nbad = _check_against_oracle(src, blocks, res, refdata, dtable0)
+    assert nbad >= len(kinds) // 2
+    # the device-resident form gives the same tensors
+    g = d.decode_blocks_dev(torch.from_numpy(src).cuda(),
+                            torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+    torch.cuda.synchronize()
+    ns = int(g["nspans"])
+    assert ns == res["spans"].size and int(g["nlines"]) == res["lines"].size
+    gres = {"spans": g["spans"][:ns].cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1),
+            "strs": g["strs"][:ns].cpu().numpy().view(qpack.SPAN_OUT_DTYPE).reshape(-1),
+            "verdict": g["verdict"][:ns].cpu().numpy(), "tokens": g["tokens"][:ns].cpu().numpy(),
+            "span_start": g["span_start"][:blocks.size + 1].cpu().numpy().view(np.uint32),
+            "status": g["status"][:blocks.size].cpu().numpy(), "dst": g["dst"].cpu().numpy()}
+    assert (gres["status"] == res["status"]).all()
+    _check_against_oracle(src, blocks, gres, refdata, dtable0)
+    lines = g["lines"][:int(g["nlines"]) * 24].cpu().numpy().view(qpack.FIELD_LINE_DTYPE)
+    assert lines.tobytes() == res["lines"].tobytes()
+
+
+def test_sections_pipeline_clean_blocks_give_the_writer_plaintext(dec0):
+    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED000A, 3000)
+    res = dec0.decode_blocks(src, blocks)
+    assert (res["status"] == 0).all()
+    assert res["lines"].size == lines.size
     pb = bytes(plain)
-    for b in np.nonzero(ok)[0][:512]:
-        ks = [int(k) for l in lines[ls[b]:ls[b + 1]] for k in (l["name"], l["value"]) if k >= 0]
-        for j, k in enumerate(range(ref_res[3][b], ref_res[3][b + 1])):
-            want = pb[strs["off"][ks[j]]:strs["off"][ks[j]] + strs["len"][ks[j]]]
-            if spans["flags"][k] & qpack.SPAN_HUFFMAN:
-                pos = int(np.searchsorted(hidx, k))
-                got = bytes(res["dst"][res["out"]["off"][pos]:res["out"]["off"][pos] + res["out"]["len"][pos]])
-            else:
-                got = bytes(src[spans["off"][k]:spans["off"][k] + spans["len"][k]])
-            assert got == want
+    ks = [int(k) for l in lines for k in (l["name"], l["value"]) if k >= 0]
+    assert len(ks) == res["spans"].size
+    for j, k in enumerate(ks):
+        o = res["strs"][j]
+        buf = res["dst"] if res["huffman"][j] else src
+        assert bytes(buf[int(o["off"]):int(o["off"]) + int(o["len"])]) == \
+            pb[int(strs["off"][k]):int(strs["off"][k]) + int(strs["len"][k])]
 
 
 def _check_cases():
     from test_http_check import cases
     return cases(0x5EED0F6, 4000)
+
+
+def test_config4_full_corpus_matches_oracle_digests(dec0):
+    """Config 4 at size: all 65,536 blocks through qh_decode_sections_batch
+    on the device (capacity 0), against the oracle's digests of every
+    decoded string, verdict and token (tests/golden/gen_golden.py)."""
+    import hashlib
+    import torch
+    from conftest import load_json
+    d = load_json("digests.json")["configs"]["c4_blocks"]
+    src, blocks, *_ = qpack.synth_field_sections(d["seed"], d["nblocks"])
+    assert hashlib.sha256(src.tobytes()).hexdigest() == d["blocks_sha256"]
+    d_src = torch.from_numpy(np.ascontiguousarray(src)).cuda()
+    g = dec0.decode_blocks_dev(d_src, torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+    torch.cuda.synchronize()
+    ns = int(g["nspans"])
+    assert ns == d["strings"] and int(g["nlines"]) == d["field_lines"]
+    assert bool((g["status"][:blocks.size] == 0).all())
+    strs = g["strs"][:ns]
+    assert bool(((strs[:, 1] >> 32) == 0).all())
+    ln = strs[:, 1] & 0xFFFFFFFF
+    tot = int(ln.sum().item())
+    assert tot == d["string_bytes"]
+    huff = ((g["spans"][:ns, 1] >> 32) & qpack.SPAN_HUFFMAN) != 0
+    pos = torch.arange(tot, device="cuda", dtype=torch.int64) - \
+        torch.repeat_interleave(torch.cumsum(ln, 0) - ln, ln)
+    at = torch.repeat_interleave(strs[:, 0], ln) + pos
+    hb = torch.repeat_interleave(huff, ln)
+    got = torch.where(hb, g["dst"][at.clamp(max=g["dst"].numel() - 1)], d_src[at.clamp(max=d_src.numel() - 1)])
+    assert hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest() == d["strings_sha256"]
+    assert hashlib.sha256(g["verdict"][:ns].cpu().numpy().tobytes()).hexdigest() == d["verdict_sha256"]
+    assert hashlib.sha256(g["tokens"][:ns].cpu().numpy().tobytes()).hexdigest() == d["token_sha256"]
 
 
 def test_check_fields_batch_host_and_device_match_scalar(dec):
@@ -118,22 +248,6 @@ def test_check_fields_batch_host_and_device_match_scalar(dec):
     qpack.check_fields_dev(dec.codec, d_src, d_sp, d_v)
     torch.cuda.synchronize()
     assert (d_v.cpu().numpy() == want).all()
-
-
-def test_decode_blocks_validates_every_string(dec):
-    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED0007, 512)
-    src = src.copy()
-    res = dec.decode_blocks(src, blocks)
-    assert (res["status"] == 0).all()
-    # synthetic names / values are alphabet A: upper-case letters make names
-    # invalid (nghttp3 rejects upper case), values are all valid
-    pb = bytes(plain)
-    names = (res["spans"]["flags"] & qpack.SPAN_NAME) != 0
-    ks = [int(k) for l in lines for k in (l["name"], l["value"]) if k >= 0]
-    for j, k in enumerate(ks):
-        s = pb[strs["off"][k]:strs["off"][k] + strs["len"][k]]
-        want = qpack.check_header_name(s) if names[j] else qpack.check_header_value(s)
-        assert res["verdict"][j] == want
 
 
 def test_lookup_tokens_batch_host_and_device_match_scalar(dec):
@@ -205,27 +319,3 @@ def test_gpu_framing_matches_host_scan_on_netbsd_and_synthetic(dec):
     _same_scan(_gpu_scan(dec, src, blocks), qpack.scan_blocks(src, blocks))
     st = _gpu_scan(dec, src, blocks)[4]
     assert (st[[11, 12]] == qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED).all() and (st[:10] == 0).all()
-
-
-def test_device_pipeline_matches_staged_path(dec):
-    import torch
-    src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED000A, 3000)
-    res = dec.decode_blocks(src, blocks)
-    d = dec.decode_blocks_dev(torch.from_numpy(np.ascontiguousarray(src)).cuda(),
-                              torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
-    torch.cuda.synchronize()
-    assert (d["status"][:blocks.size].cpu().numpy() == res["status"]).all()
-    assert d["nspans"] == res["spans"].size
-    nh = d["nhuff"]
-    assert nh == res["huffman"].sum()
-    out = d["out"][:nh].cpu().numpy()
-    dst = d["dst"].cpu().numpy()
-    ho = res["out"]
-    for k in range(ho.size):
-        a = bytes(res["dst"][ho["off"][k]:ho["off"][k] + ho["len"][k]])
-        b = bytes(dst[out[k, 0]:out[k, 0] + (out[k, 1] & 0xFFFFFFFF)])
-        assert a == b
-    assert (d["verdict"][:nh].cpu().numpy() == res["verdict"][res["huffman"]]).all()
-    sel = d["name_sel"].cpu().numpy()
-    names = [bytes(dst[o:o + (l & 0xFFFFFFFF)]) for o, l in out[sel]]
-    assert (d["tokens"][:nh].cpu().numpy()[sel] == [qpack.lookup_token(x) for x in names]).all()

@@ -202,12 +202,65 @@ def test_c_scanner_matches_oracle_on_synthetic_sections_and_errors():
         b"\x00\x00\x50\x7f\x81\x80\x04" + b"a" * 10,        # value 65536+1... truncated
         b"\x00\x00\xd1", b"\x00\x00\x10", b"\x00\x00\x00\x00",
     ]
+    cases += [b"\x00\x00" + ref.write_indexed(0xC0, rng.randrange(99, 300), 6) for _ in range(4)]
     for sec in cases:
         st, prefix, lines, spans = qpack.scan_field_section(sec, 7)
         rst, rprefix, rlines, rspans = ref.scan_field_section(sec, 7)
         assert st == rst, sec
         assert prefix == rprefix
         assert _tuples(lines, spans) == (rlines, rspans)
+
+
+def test_table_free_index_checks_match_oracle():
+    """Checks brel2abs / pbrel2abs / validate_index / the sign rule make
+    whatever the dynamic table holds (qpack.c:3414-3418, :3971-4017,
+    :2787-2798)."""
+    bad = qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED
+    v = ref.write_indexed_name(0x50, 3, 4, b"abc")
+    cases = {
+        b"\x00\x00" + ref.write_indexed(0xC0, 98, 6): 0,        # last static entry
+        b"\x00\x00" + ref.write_indexed(0xC0, 99, 6): bad,      # past the static table
+        b"\x00\x00" + ref.write_indexed_name(0x50, 99, 4, b"x"): bad,
+        b"\x00\x00" + ref.write_indexed_name(0x50, 200, 4, b"x"): bad,
+        b"\x00\x00" + ref.write_indexed(0x80, 0, 6): bad,       # dynamic, ricnt 0
+        b"\x00\x00" + ref.write_indexed(0x10, 0, 4): bad,       # post-base, ricnt 0
+        b"\x00\x00" + ref.write_indexed_name(0x40, 0, 4, b"x"): bad,
+        b"\x00\x00" + ref.write_indexed_name(0x00, 0, 3, b"x"): bad,
+        b"\x00\x80" + v: bad,                                     # sign with ricnt 0
+        b"\x02\x80" + v: 0,                                       # needs table state
+        b"\x02\x00" + ref.write_indexed(0x80, 0, 6): 0,         # dynamic, ricnt > 0
+        b"\x00\x00" + v + ref.write_indexed(0xC0, 120, 6): bad,  # after a good line
+    }
+    for sec, want in cases.items():
+        st, _, lines, spans = qpack.scan_field_section(sec)
+        rst, _, rlines, rspans = ref.scan_field_section(sec)
+        assert st == rst == want, sec
+        assert _tuples(lines, spans) == (rlines, rspans)
+    # the failed block keeps the string read before the error (its value)
+    st, _, lines, spans = qpack.scan_field_section(b"\x00\x00" + v + ref.write_indexed(0xC0, 120, 6))
+    assert st == bad and lines.size == 0 and spans.size == 1
+    # capacity 0 (config 4): any Required Insert Count but 0 fails
+    assert ref.scan_field_section(b"\x02\x00" + v, dtable0=True)[0] == bad
+    assert ref.scan_field_section(b"\x00\x00" + v, dtable0=True)[0] == 0
+    # encoder stream: a static name reference must be < 99 (rel2abs)
+    es = ref.write_indexed_name(0xC0, 99, 6, b"v")
+    assert qpack.scan_encoder_stream(es)[0] == ref.scan_encoder_stream(es)[0] == \
+        qpack.QH_ERR_QPACK_ENCODER_STREAM_ERROR
+    es = ref.write_indexed_name(0xC0, 98, 6, b"v")
+    assert qpack.scan_encoder_stream(es)[0] == ref.scan_encoder_stream(es)[0] == len(es)
+
+
+def test_decode_field_section_error_order():
+    """A Huffman string that fails before a framing error decides the block
+    (-401, qpack.c:3604-3609), as the streaming reference meets it first."""
+    bad_h = b"\x81\x00"          # H=1, 1 byte, zero padding: -108
+    too_big = ref.put_varint(65537, 7) + b"a" * 65537
+    sec = b"\x00\x00\x50" + bad_h + b"\x50" + too_big
+    assert ref.scan_field_section(sec)[0] == qpack.QH_ERR_QPACK_HEADER_TOO_LARGE
+    st, lines, spans, strings = ref.decode_field_section(sec)
+    assert st == qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED and strings == [None]
+    sec = b"\x00\x00\x50\x03abc\x50" + too_big
+    assert ref.decode_field_section(sec)[0] == qpack.QH_ERR_QPACK_HEADER_TOO_LARGE
 
 
 def test_value_too_large_is_header_too_large():
