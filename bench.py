@@ -53,9 +53,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1 << 20, help="strings per GPU (config 3)")
-    ap.add_argument("--lo", type=int, default=8)
-    ap.add_argument("--hi", type=int, default=256)
+    # (no option may be a prefix of a torch.distributed.run option: --n, --lo ...)
+    ap.add_argument("--strings", type=int, default=1 << 20, help="strings per GPU (config 3)")
+    ap.add_argument("--min-len", type=int, default=8)
+    ap.add_argument("--max-len", type=int, default=256)
     ap.add_argument("--alphabet", choices=["A", "U"], default="A")
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0003)
     ap.add_argument("--c5-strings", type=int, default=16 << 20, help="config 5: strings in all")
@@ -203,7 +204,7 @@ def main():
         return enc, eout, int(elen.sum().item()), dec, dout
 
     # ---- config 3: one global batch of world x n strings, split by bytes ----
-    lens_all = synth.lengths(args.seed, args.n * world, args.lo, args.hi)
+    lens_all = synth.lengths(args.seed, args.strings * world, args.min_len, args.max_len)
     b0, b1 = shard.split_by_bytes(lens_all, world)[rank]
     first = int(lens_all[:b0].sum(dtype=np.uint64))
     my_ln = lens_all[b0:b1]
@@ -324,13 +325,13 @@ def main():
     # ---- alphabet U (config 3 shape), rank 0 alone ----
     configU = None
     if rank == 0 and world == 1 and not args.no_configs:
-        u_src, u_spans, u_total = codec.synth(args.seed, args.n, args.lo, args.hi, synth.ALPHABET_U)
+        u_src, u_spans, u_total = codec.synth(args.seed, args.strings, args.min_len, args.max_len, synth.ALPHABET_U)
         u_enc, u_eout, u_eb, u_dec, u_dout = buffers(u_src, u_spans)
         codec.decode_dev(u_enc, u_eout, u_dec, u_dout)
         u_ok = roundtrip_ok(u_src, u_spans, u_dec, u_dout)
         tue = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 5)
         tud = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 5)
-        configU = {"strings": args.n, "plain_bytes": u_total, "enc_bytes": u_eb,
+        configU = {"strings": args.strings, "plain_bytes": u_total, "enc_bytes": u_eb,
                    "encode_GiBps": round(u_total / tue / GIB, 2),
                    "decode_GiBps": round(u_total / tud / GIB, 2),
                    "round_trip_GiBps": round(u_total / (tue + tud) / GIB, 2), "bit_exact": u_ok}
@@ -361,9 +362,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64, nghttp3_amd/synth.py)",
             "config": {"workload": "config 3: Huffman encode+decode round trip, 2^20 strings "
-                                   f"{args.lo}-{args.hi} B per GPU, alphabet {args.alphabet}; one "
+                                   f"{args.min_len}-{args.max_len} B per GPU, alphabet {args.alphabet}; one "
                                    "batch of N x 2^20 strings split by bytes over the N GPUs",
-                       "strings_per_gpu": args.n, "strings_rank0": n, "plain_bytes_rank0": total,
+                       "strings_per_gpu": args.strings, "strings_rank0": n, "plain_bytes_rank0": total,
                        "enc_bytes_rank0": enc_bytes, "plain_bytes_all": int(total_all),
                        "seed": hex(args.seed), "parallelism": f"shard{world}",
                        "dist_backend": args.dist_backend if world > 1 else None},
@@ -402,6 +403,11 @@ def leg_config4(args, torch, dev, codec, D, rank, world, timed):
     bufs = fsd.decode_blocks_dev(d_src, d_blk)
     torch.cuda.synchronize()
     t_pipe = timed(lambda: fsd.decode_blocks_dev(d_src, d_blk, bufs), args.steps)
+    codec.enable_timing(True)
+    for _ in range(3):
+        fsd.decode_blocks_dev(d_src, d_blk, bufs)
+    kt = {k: round(ms / max(c, 1) * 1e3, 2) for k, (c, ms) in codec.kernel_times().items()}
+    codec.enable_timing(False)
     # bit-exact: every string (Huffman ones from dst, raw ones in place) in
     # span order equals the plaintext the writer was given
     ns = int(bufs["nspans"])
@@ -445,6 +451,7 @@ def leg_config4(args, torch, dev, codec, D, rank, world, timed):
             "gpu_pipeline_huffman_GiBps": round(h_all / t_pipe / GIB, 2),
             "gpu_pipeline_block_GBps": round(blk_all / t_pipe / 1e9, 2),
             "valid_strings_rank0": valid,
+            "kernel_avg_us_rank0": kt,
             "host_path_ms": round(t_host * 1e3, 3),
             "host_path_blocks_per_s": round(nb_all / t_host, 1),
             "bit_exact": D.sum(0.0 if ok else 1.0) == 0,

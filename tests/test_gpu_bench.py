@@ -17,7 +17,7 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 def test_bench_two_ranks_rehearsal():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-           "--one-device", "--n", "65536", "--steps", "2", "--warmup", "1",
+           "--one-device", "--strings", "65536", "--steps", "2", "--warmup", "1",
            "--c5-strings", "200000", "--c4-blocks", "2000", "--no-cpu-baseline", "--no-host-path"]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
