@@ -155,6 +155,14 @@ typedef struct qh_ctx qh_ctx;
 QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream);
 QH_EXPORT void qh_ctx_del(qh_ctx *ctx);
 QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
+/* Decoder kernel of qh_decode_batch (results are identical; speed is not):
+ * QH_DECODER_WINDOWS (default) sorts 256-string windows by length and
+ * decodes a window per workgroup -- fastest for strings of similar length
+ * (headers of 8-256 B); QH_DECODER_QUEUE lets every wave take strings from
+ * its own queue -- fastest for skewed lengths (Zipf up to 4 KiB). */
+#define QH_DECODER_WINDOWS 0
+#define QH_DECODER_QUEUE 1
+QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 QH_EXPORT void *qh_ctx_stream(qh_ctx *ctx);
 /* Wait for all work queued on the context's stream. */
 QH_EXPORT int qh_ctx_sync(qh_ctx *ctx);

@@ -5,17 +5,19 @@
 // header-field strings.  Integer/byte work only: no MFMA.  Design notes and
 // the roofline accounting are in DESIGN.md.
 //
-// Kernels (all launched on the context's stream):
-//   qh_k_dec_reserve   per block: output slot bytes of its strings
-//   qh_k_dec_lanes     decode, one string per lane, 4-bit FSM in LDS
-//                      (huffman.c:103-114)
-//   qh_k_dec_lut       decode, one string per lane, 12-bit multi-symbol table
-//                      (opt-in: QHUFF_DECODER=lut)
-//   qh_k_enc_lens      encoded length per string (huffman.c:34-43), chunk
-//                      engine, + per-block totals
+// Shipped kernels (all launched on the context's stream):
+//   qh_k_dec_reserve + qh_k_dec_peek   decode, sorted 256-string windows, a
+//                      W-bit table lookup per code (huffman.c:87-124)
+//   qh_k_dec_wres + qh_k_dec_q         decode, per-wave string queues
+//   qh_k_enc_lens_stream / _lane       encoded lengths (huffman.c:34-43)
 //   qh_k_enc_lanes     codes, one string per lane, dense output through an
 //                      LDS stage (huffman.c:45-78)
-//   qh_k_scan, qh_k_synth_*   synthetic inputs (bench/tests only)
+//   qh_k_frame_*, qh_k_sections_post, qh_k_check_fields,
+//   qh_k_lookup_tokens QPACK framing, validation and tokens
+//   qh_k_scan, qh_k_synth_*   prefix sums, synthetic inputs (bench/tests)
+// Development variants (decoders fsm / fsm2 / lut / run / other peek
+// widths, the chunk-engine and streaming encoders) build only with
+// -DQH_DEV_VARIANTS (make dev -> libqhuff_dev.so).
 
 #include <hip/hip_runtime.h>
 
@@ -37,13 +39,21 @@
 #include "qh_common.h"      // span/stat types, tables, small helpers
 #include "qh_chunk.inc"      // block ranges, windows, chunk rounds, scans
 #include "qh_scan.inc"       // batch prefix sum (synthetic inputs)
+#include "qh_dec_common.inc"  // decode table blob, slot reservation
+#ifdef QH_DEV_VARIANTS         // development variants (make dev): not shipped
 #include "qh_lane_dec.inc"   // decoder: 4-bit FSM, one string per lane
 #include "qh_lane_dec2.inc"  // decoder: 4-bit FSM, two strings per lane
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
-#include "qh_peek_dec.inc"   // decoder: W-bit peek table, lock-step lanes
-#include "qh_dec3.inc"       // decoder (default): plan + task-queue lanes
-#include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes, chunks), codes (lanes)
-#include "qh_enc_stream.inc" // encoder (default codes): streaming region rounds
+#endif
+#include "qh_peek_dec.inc"   // decoder (default): W-bit peek table, sorted windows
+#ifdef QH_DEV_VARIANTS
+#include "qh_dec3.inc"       // decoder: plan + task-queue lanes
+#endif
+#include "qh_dec_q.inc"      // decoder: per-wave string queues (QH_DECODER_QUEUE)
+#include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes)
+#ifdef QH_DEV_VARIANTS
+#include "qh_enc_stream.inc" // encoder codes: streaming region rounds
+#endif
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
 #include "qh_api.inc"    // host API (include/qhuff.h)
 #include "qh_validate.inc"  // field name / value validation batch, header-name tokens

@@ -167,6 +167,12 @@ class HuffmanBatchCodec:
             pass
 
     # -- context utilities --------------------------------------------------
+    def set_decoder(self, kind: str):
+        """'windows' (default: strings of similar length) or 'queue' (skewed
+        lengths, e.g. Zipf up to 4 KiB); results are identical."""
+        k = {"windows": _lib.QH_DECODER_WINDOWS, "queue": _lib.QH_DECODER_QUEUE}[kind]
+        _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
+
     def sync(self):
         _lib.check(self._lib.qh_ctx_sync(self._ctx), "qh_ctx_sync")
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Time every decoder variant (QHUFF_DECODER) on a BASELINE-shaped batch and
-check each against the plaintext (development tool, one GPU).
+check each against the plaintext (development tool, one GPU).  Loads the
+development build (make dev -> nghttp3_amd/lib/libqhuff_dev.so), which holds
+every variant; the product library ships peek11lda and q1w4r4 only.
 
 Usage: python scripts/dec_variants.py [--n N] [--alphabet A|U] [--reps R]
          [--kinds fsm,peek11,...]
@@ -14,6 +16,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("QHUFF_LIB", os.path.join(ROOT, "nghttp3_amd", "lib", "libqhuff_dev.so"))
 
 
 def main():
@@ -23,7 +26,8 @@ def main():
     ap.add_argument("--hi", type=int, default=256)
     ap.add_argument("--alphabet", default="A")
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--kinds", default="peek11lda,peek11ld,peek11")
+    ap.add_argument("--kinds", default="q1w4r4,peek11lda")
+    ap.add_argument("--zipf", action="store_true", help="config 5 lengths (Zipf 1..4096)")
     args = ap.parse_args()
     import torch
     from nghttp3_amd import HuffmanBatchCodec, synth
@@ -31,7 +35,12 @@ def main():
 
     alph = synth.ALPHABET_A if args.alphabet == "A" else synth.ALPHABET_U
     base = HuffmanBatchCodec(device=0)
-    src, spans, total = base.synth(0x5EED0003, args.n, args.lo, args.hi, alph)
+    if args.zipf:
+        zl = synth.zipf_lengths(0x5EED0005, args.n, 1, 4096, 1.2)
+        spans, total = base.spans_to_device(zl)
+        src = base.synth_fill(0x5EED0005, 0, total, alph)
+    else:
+        src, spans, total = base.synth(0x5EED0003, args.n, args.lo, args.hi, alph)
     n = args.n
     ln = spans[:, 1] & 0xFFFFFFFF
     bound = int(((ln * 30 + 7) // 8).sum().item())
@@ -63,7 +72,7 @@ def main():
             ok = bool((dec[rep_d + pos] == src[:total]).all())
         ks = {k: round(ms / max(cnt, 1) * 1e3, 2) for k, (cnt, ms) in kt.items()}
         main_us = max(ks.values())
-        print(json.dumps({"kind": kind, "alphabet": args.alphabet, "n": n, "kernels_us": ks,
+        print(json.dumps({"kind": kind, "alphabet": args.alphabet, "zipf": args.zipf, "n": n, "kernels_us": ks,
                           "plain_GiBps": round(total / (main_us * 1e-6) / 2**30, 1),
                           "algo_GBps": round((total + ebytes + 32 * n) / (main_us * 1e-6) / 1e9, 1),
                           "bit_exact": ok}), flush=True)

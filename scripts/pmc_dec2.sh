@@ -1,0 +1,18 @@
+#!/bin/bash
+# SQ counters of two decoder variants (one rocprofv3 --pmc pass per group).
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1; KINDS=${2:-q1w4,peek11lda}
+OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for group in \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
+  "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_SMEM" ; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $group --output-format csv -d "$OUT/g$i" -o run -- \
+     python3 "$ROOT/scripts/dec_variants.py" --kinds "$KINDS" --reps 2 > "$OUT/g$i.log" 2>&1
+  rc=$?; echo "group $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/g$i.log"; exit $rc; fi
+done
+python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E 'dec_q|dec_peek' | tr ' ' '\n'

@@ -214,10 +214,21 @@ def test_synth_device_matches_host(codec):
     assert (src.cpu().numpy()[:total] == plain).all()
 
 
-@pytest.mark.parametrize("name", ["c2_A", "c2_U", "c3_A"])
-def test_full_size_config(codec, digests, name):
+@pytest.mark.parametrize("name,decoder", [("c2_A", "windows"), ("c2_U", "windows"),
+                                          ("c3_A", "windows"), ("c3_A", "queue"),
+                                          ("c2_U", "queue")])
+def test_full_size_config(codec, digests, name, decoder):
     """BASELINE configs at full size (2^20 strings): synth digest, encode
-    digest vs the oracle's, then decode round trip (size-independent)."""
+    digest vs the oracle's, then decode round trip (size-independent), with
+    either shipped decoder."""
+    codec.set_decoder(decoder)
+    try:
+        _full_size_config(codec, digests, name)
+    finally:
+        codec.set_decoder("windows")
+
+
+def _full_size_config(codec, digests, name):
     torch = torch_mod()
     d = digests[name]
     alph = synth.ALPHABET_A if d["alphabet"] == "A" else synth.ALPHABET_U
@@ -254,11 +265,20 @@ def test_full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
-def test_config5_rank_shard_full_size(codec, digests):
+@pytest.mark.parametrize("decoder", ["windows", "queue"])
+def test_config5_rank_shard_full_size(codec, digests, decoder):
     """Config 5 at size: rank 0's shard of 16M Zipf strings split by bytes
     over 8 GPUs (2.1M strings, 438 MB, lengths 1..4096), as bench.py cuts
     it: the device generator from the global byte offset, encode digests vs
     the oracle's, then the decode round trip (chunked compare)."""
+    codec.set_decoder(decoder)
+    try:
+        _config5_rank_shard(codec, digests)
+    finally:
+        codec.set_decoder("windows")
+
+
+def _config5_rank_shard(codec, digests):
     from nghttp3_amd import shard
     torch = torch_mod()
     d = digests["c5_r0of8"]
@@ -408,29 +428,23 @@ def test_encode_dst_cap_too_small(codec, corpus):
         assert d[o[j]:o[j] + l[j]].tobytes() == want
 
 
-DECODERS = ["run", "fsm", "lut", "fsm2", "peek11ld", "peek11lda", "peek11", "peek11d", "peek10", "peek12",
-            "peek11_8", "peek11_2", "peek11_2w5", "snake11d", "peek10ld"]
+# The two shipped decoders (qh_ctx_set_decoder); the development variants
+# (make dev) are timed by scripts/dec_variants.py, not shipped.
+DECODERS = ["windows", "queue"]
 
 
 def codec_of(kind):
-    import os
     from nghttp3_amd import HuffmanBatchCodec
-    old = os.environ.get("QHUFF_DECODER")
-    os.environ["QHUFF_DECODER"] = kind
-    try:
-        return HuffmanBatchCodec(device=0)
-    finally:
-        if old is None:
-            del os.environ["QHUFF_DECODER"]
-        else:
-            os.environ["QHUFF_DECODER"] = old
+    c = HuffmanBatchCodec(device=0)
+    c.set_decoder(kind)
+    return c
 
 
 @pytest.mark.parametrize("kind", DECODERS)
 def test_decoder_variants(kind, corpus, errors, kat, codec):
-    """Every decoder (the 4-bit FSM, QHUFF_DECODER=lut -- the 12-bit table,
-    fsm2 -- two strings per lane, peekW -- W-bit peek table in lock-step)
-    gives the oracle's bytes and statuses: golden corpus, corrupted strings,
+    """Both decoders (the window decoder: sorted 256-string windows, W-bit
+    peek table in lock-step; the queue decoder: per-wave string queues)
+    give the oracle's bytes and statuses: golden corpus, corrupted strings,
     the reference's error verdicts, RFC vectors, and mixed lengths 0-5000 B
     over alphabet A and all 256 byte values (long codes, EOS-prefix ends)."""
     c = codec_of(kind)
@@ -485,23 +499,16 @@ def test_decoder_variants(kind, corpus, errors, kat, codec):
         c.close()
 
 
-@pytest.mark.parametrize("mode", ["default", "lane", "chunks", "streamcodes", "streamcodes_lane",
-                                  "streamcodes_listed"])
+@pytest.mark.parametrize("mode", ["default", "lane"])
 def test_encode_length_passes(mode, corpus, digests):
     """The encoder's passes: streaming lengths + lane-per-string codes
-    (default), every window's lengths left to the lane-per-string pass
-    (QHUFF_DEBUG=4), the chunk-engine lengths (QHUFF_ENCODER=chunks), the
-    streaming codes kernel (QHUFF_CODES=stream) alone, with lane lengths, and
-    with every window listed to the lane codes pass (QHUFF_DEBUG=8) --
-    corpus lengths/codes, counts, overlapping and scattered spans, and the
+    (default), and every window's lengths left to the lane-per-string pass
+    (QHUFF_DEBUG=4) -- corpus lengths/codes, counts, overlapping and scattered spans, and the
     full-size c2_U digest."""
     import os
     from nghttp3_amd import HuffmanBatchCodec
-    env = {"default": {}, "lane": {"QHUFF_DEBUG": "4"},
-           "chunks": {"QHUFF_ENCODER": "chunks"}, "streamcodes": {"QHUFF_CODES": "stream"},
-           "streamcodes_lane": {"QHUFF_CODES": "stream", "QHUFF_DEBUG": "4"},
-           "streamcodes_listed": {"QHUFF_CODES": "stream", "QHUFF_DEBUG": "8"}}[mode]
-    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG", "QHUFF_ENCODER", "QHUFF_CODES")}
+    env = {"default": {}, "lane": {"QHUFF_DEBUG": "4"}}[mode]
+    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG",)}
     for k in old:
         os.environ.pop(k, None)
     os.environ.update(env)
