@@ -13,7 +13,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 CFLAGS   := -std=c11 -O2 -fPIC -fvisibility=hidden -Wall -Wextra
 
-all: $(LIB) $(ARCHIVE) $(ORACLE)
+DRIVER  := $(LIBDIR)/qpack
+
+all: $(LIB) $(ARCHIVE) $(DRIVER) $(ORACLE)
 
 $(CSRC)/qh_tables.h: nghttp3_amd/tools/gen_tables.py
 	python3 nghttp3_amd/tools/gen_tables.py $@
@@ -30,16 +32,26 @@ $(LIBDIR)/qh_qpack.o: $(CSRC)/qh_qpack.c $(CSRC)/qh_qpack_core.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
+$(LIBDIR)/qh_static.o: $(CSRC)/qh_static.c include/qhuff.h
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -c $< -o $@
+
 $(LIBDIR)/qh_http.o: $(CSRC)/qh_http.c $(CSRC)/qh_tokens.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+$(LIB): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# The QIF bench driver (examples/qpack.cc counterpart), linked against the
+# shared library next to it.
+$(DRIVER): $(CSRC)/qh_qif.cc include/qhuff.h $(LIB)
+	$(CXX) -std=c++17 -O2 -Wall -Wextra -o $@ $< -L$(LIBDIR) -lqhuff \
+	  -Wl,-rpath,'$$ORIGIN' -Wl,-rpath-link,/opt/rocm/lib
 
 # Static archive of the same two objects, for linking into libnghttp3 in
 # place of the reference's Huffman objects.
-$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+$(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	rm -f $@
 	ar rcs $@ $^
 
@@ -47,9 +59,9 @@ $(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(L
 # points at it).
 STAMPS := $(LIBDIR)/libqhuff_stamps.so
 stamps: $(STAMPS)
-$(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+$(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -DQH_DEV_VARIANTS -c $< -o $(LIBDIR)/qh_device_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_stamps.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_stamps.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
 # Development build with every kernel variant (-DQH_DEV_VARIANTS: decoders
 # fsm / fsm2 / lut / run / other peek widths and queue shapes, the
@@ -58,9 +70,9 @@ $(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_
 # (scripts/dec_variants.py).
 DEV := $(LIBDIR)/libqhuff_dev.so
 dev: $(DEV)
-$(DEV): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+$(DEV): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_DEV_VARIANTS -c $< -o $(LIBDIR)/qh_device_dev.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_dev.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_dev.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
 # Oracle: -O2 -mavx2 as nghttp3's README.rst:61-67 prescribes for the
 # reference build (the Huffman loop itself has no SIMD path).
@@ -68,6 +80,6 @@ $(ORACLE): oracle/qh_oracle.c oracle/qh_oracle.h
 	$(CC) -std=c11 -O2 -mavx2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIB) $(ARCHIVE) $(STAMPS) $(DEV) $(ORACLE)
+	rm -f $(LIBDIR)/*.o $(DRIVER) $(LIB) $(ARCHIVE) $(STAMPS) $(DEV) $(ORACLE)
 
 .PHONY: all clean stamps

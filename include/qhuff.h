@@ -365,6 +365,9 @@ typedef struct qh_sections {
   uint32_t *line_start; /* nblocks + 1 */
   uint32_t *span_start; /* nblocks + 1 */
   int32_t *status;      /* nblocks     */
+  qh_section_prefix *prefixes; /* nblocks, optional: each block's prefix as
+                                  encoded (zero for a block whose prefix
+                                  does not parse) */
   uint8_t *dst;
   uint64_t dst_cap;
   /* filled in by the call */
@@ -428,6 +431,52 @@ QH_EXPORT int qh_qpack_write_sections(const uint8_t *plain,
                                       const qh_section_prefix *prefixes,
                                       uint8_t *dst, size_t dst_cap,
                                       qh_span_in *sections);
+
+/* ---- The encoder side of whole field sections (SURVEY.md section 8(a)
+ * rows a9 / a10, 8(f) row 2) ----------------------------------------------
+ * The static table (RFC 9204 Appendix A; the reference's stable[],
+ * qpack.c:189-291): entry idx's name and value (static storage). */
+QH_EXPORT int qh_qpack_static_entry(size_t idx, const uint8_t **name,
+                                    size_t *namelen, const uint8_t **value,
+                                    size_t *valuelen);
+
+/* The representation nghttp3_qpack_encoder_encode_nv (qpack.c:1455-1628)
+ * chooses for each of nfields fields when the dynamic table is not used
+ * (capacity 0; qpack_encode -s 0): field i is strs[2i] (name) and
+ * strs[2i + 1] (value), spans of `plain`; never[i] (optional) is its
+ * NGHTTP3_NV_FLAG_NEVER_INDEX.  lines[i] becomes an Indexed Field Line
+ * (static entry with that name and value), a Literal With (static) Name
+ * Reference, or a Literal With Literal Name, with name / value = 2i / 2i + 1
+ * where used and QH_FL_NEVER from never[i] (the static lookup also skips the
+ * value match for authorization and cookie values under 20 bytes,
+ * :1307-1321, :1643-1645).  Host C. */
+QH_EXPORT int qh_qpack_plan_fields(const uint8_t *plain, const qh_span_in *strs,
+                                   size_t nfields, const uint8_t *never,
+                                   qh_field_line *lines);
+
+/* Batch writer of whole field sections on the GPU: the encoder batch
+ * adapter of the Huffman call sites (qpack.c:1851-2006).  Section b is
+ * lines [line_start[b], line_start[b + 1]) after its prefix (prefixes[b], or
+ * all zero when prefixes is NULL: no dynamic-table references); a line's
+ * name / value index strs, spans of plain.  Steps: hlen of every string
+ * (the count kernels), Huffman iff hlen < len (:1862, :1954, :1962), the
+ * picked strings encoded densely (the encode kernels), then the sections
+ * written (first bytes and prefixes as qh_qpack_write_sections; byte for
+ * byte its output).  sections[b] receives (off, len) in dst, sections back
+ * to back from 0; *dst_need the total.  All pointers in HBM
+ * (QH_WHERE_DEVICE; one sync, for the caps check) or in host memory
+ * (QH_WHERE_HOST: staged, blocking).  Returns 0, QH_ERR_NOMEM (dst_cap <
+ * *dst_need; nothing written), QH_ERR_INVALID_ARGUMENT (unknown opcode or
+ * missing string) or QH_ERR_FATAL. */
+QH_EXPORT int qh_encode_sections_batch(qh_ctx *ctx, const uint8_t *plain,
+                                       const qh_span_in *strs, size_t nstrs,
+                                       const qh_field_line *lines,
+                                       const uint32_t *line_start,
+                                       size_t nsections,
+                                       const qh_section_prefix *prefixes,
+                                       uint8_t *dst, uint64_t dst_cap,
+                                       qh_span_in *sections,
+                                       uint64_t *dst_need, int where);
 
 /* ---- Field name / value validation -------
  * Scalar drop-ins for the public functions (nghttp3.h:3443, :3452;

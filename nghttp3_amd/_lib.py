@@ -96,6 +96,9 @@ EXPORTED_FUNCTIONS = (
     "qh_qpack_scan_blocks",
     "qh_scan_blocks_batch",
     "qh_decode_sections_batch",
+    "qh_encode_sections_batch",
+    "qh_qpack_static_entry",
+    "qh_qpack_plan_fields",
     "qh_qpack_scan_encoder_stream",
     "qh_qpack_put_varint_len",
     "qh_qpack_put_varint",

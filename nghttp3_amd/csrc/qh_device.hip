@@ -14,6 +14,7 @@
 //                      LDS stage (huffman.c:45-78)
 //   qh_k_frame_*, qh_k_sections_post, qh_k_check_fields,
 //   qh_k_lookup_tokens QPACK framing, validation and tokens
+//   qh_k_encsec_*      representation writer of whole field sections
 //   qh_k_scan, qh_k_synth_*   prefix sums, synthetic inputs (bench/tests)
 // Development variants (decoders fsm / fsm2 / lut / run / other peek
 // widths, the chunk-engine and streaming encoders) build only with
@@ -59,4 +60,5 @@
 #include "qh_validate.inc"  // field name / value validation batch, header-name tokens
 #include "qh_frame.inc"     // QPACK field-section framing on the device
 #include "qh_sections.inc"  // whole field sections: frame -> decode -> fold / check / tokens
+#include "qh_enc_sections.inc"  // whole field sections out: count -> pick -> encode -> write
 

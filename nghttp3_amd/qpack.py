@@ -39,6 +39,10 @@ FIELD_LINE_DTYPE = np.dtype([("index", "<u8"), ("opcode", "u1"), ("flags", "u1")
 assert FIELD_LINE_DTYPE.itemsize == 24
 
 
+PREFIX_DTYPE = np.dtype([("ricnt", "<u8"), ("delta_base", "<u8"), ("sign", "<u4"),
+                         ("reserved", "<u4")])
+
+
 class qh_section_prefix(ctypes.Structure):
     _fields_ = [("ricnt", ctypes.c_uint64), ("delta_base", ctypes.c_uint64),
                 ("sign", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
@@ -54,7 +58,7 @@ class qh_sections(ctypes.Structure):
                 ("strs", ctypes.c_void_p), ("verdict", ctypes.c_void_p),
                 ("token", ctypes.c_void_p), ("line_start", ctypes.c_void_p),
                 ("span_start", ctypes.c_void_p), ("status", ctypes.c_void_p),
-                ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_uint64),
+                ("prefixes", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_uint64),
                 ("nlines", ctypes.c_uint64), ("nspans", ctypes.c_uint64),
                 ("nhuff", ctypes.c_uint64), ("dst_need", ctypes.c_uint64)]
 
@@ -106,6 +110,14 @@ def _load():
         lib.qh_decode_sections_batch.argtypes = [vp, vp, vp, sz, c.c_uint32, c.POINTER(qh_sections),
                                                  i32]
         lib.qh_decode_sections_batch.restype = i32
+        lib.qh_qpack_static_entry.argtypes = [sz, c.POINTER(vp), c.POINTER(sz), c.POINTER(vp),
+                                              c.POINTER(sz)]
+        lib.qh_qpack_static_entry.restype = i32
+        lib.qh_qpack_plan_fields.argtypes = [vp, vp, sz, vp, vp]
+        lib.qh_qpack_plan_fields.restype = i32
+        lib.qh_encode_sections_batch.argtypes = [vp, vp, vp, sz, vp, vp, sz, vp, vp, u64, vp,
+                                                 c.POINTER(u64), i32]
+        lib.qh_encode_sections_batch.restype = i32
         _L = lib
     return _L
 
@@ -387,7 +399,7 @@ class FieldSectionDecoder:
         for _ in range(2):  # a second try only when dst was too small
             st = qh_sections(p(b["lines"]), cap, p(b["spans"]), cap, p(b["strs"]), p(b["verdict"]),
                              p(b["tokens"]), p(b["line_start"]), p(b["span_start"]), p(b["status"]),
-                             p(b["dst"]), b["dst"].numel(), 0, 0, 0, 0)
+                             None, p(b["dst"]), b["dst"].numel(), 0, 0, 0, 0)
             rv = lib.qh_decode_sections_batch(self.codec._ctx, ctypes.c_void_p(src.data_ptr()),
                                               ctypes.c_void_p(blocks.data_ptr()), n, self.opts,
                                               ctypes.byref(st), _lib.QH_WHERE_DEVICE)
@@ -420,11 +432,13 @@ class FieldSectionDecoder:
         ls = np.zeros(n + 1, dtype=np.uint32)
         ss = np.zeros(n + 1, dtype=np.uint32)
         status = np.zeros(max(n, 1), dtype=np.int32)
+        prefixes = np.zeros(max(n, 1), dtype=PREFIX_DTYPE)
         dst = np.zeros(64, dtype=np.uint8)
         for _ in range(2):
             st = qh_sections(lines.ctypes.data, cap, spans.ctypes.data, cap, strs.ctypes.data,
                              verdict.ctypes.data, tokens.ctypes.data, ls.ctypes.data, ss.ctypes.data,
-                             status.ctypes.data, dst.ctypes.data, dst.size, 0, 0, 0, 0)
+                             status.ctypes.data, prefixes.ctypes.data, dst.ctypes.data, dst.size,
+                             0, 0, 0, 0)
             rv = lib.qh_decode_sections_batch(self.codec._ctx, _vp(src), _vp(blocks), n, self.opts,
                                               ctypes.byref(st), _lib.QH_WHERE_HOST)
             if rv == _lib.QH_ERR_NOMEM and st.dst_need > dst.size:
@@ -437,4 +451,83 @@ class FieldSectionDecoder:
         return {"lines": lines[:st.nlines], "spans": spans, "strs": strs[:ns],
                 "huffman": (spans["flags"] & SPAN_HUFFMAN) != 0, "verdict": verdict[:ns],
                 "tokens": tokens[:ns], "line_start": ls, "span_start": ss, "status": status[:n],
-                "dst": dst}
+                "prefixes": prefixes[:n], "dst": dst}
+
+
+def static_entry(idx: int):
+    """qh_qpack_static_entry: (name, value) of static table entry idx."""
+    lib = _load()
+    n, v = ctypes.c_void_p(), ctypes.c_void_p()
+    nl, vl = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(lib.qh_qpack_static_entry(idx, ctypes.byref(n), ctypes.byref(nl), ctypes.byref(v),
+                                         ctypes.byref(vl)), "qh_qpack_static_entry")
+    return ctypes.string_at(n, nl.value), ctypes.string_at(v, vl.value) if vl.value else b""
+
+
+def plan_fields(plain, strs, never=None):
+    """qh_qpack_plan_fields: fields (strs[2i], strs[2i+1]) of plain -> the
+    field lines the reference encoder writes at dynamic table capacity 0."""
+    lib = _load()
+    plain = _u8(plain)
+    if plain.size == 0:
+        plain = np.zeros(1, dtype=np.uint8)
+    strs = np.ascontiguousarray(strs, dtype=SPAN_IN_DTYPE)
+    nf = strs.size // 2
+    lines = np.zeros(max(nf, 1), dtype=FIELD_LINE_DTYPE)
+    nv = None if never is None else np.ascontiguousarray(never, dtype=np.uint8)
+    _lib.check(lib.qh_qpack_plan_fields(_vp(plain), _vp(strs), nf, None if nv is None else _vp(nv),
+                                        _vp(lines)), "qh_qpack_plan_fields")
+    return lines[:nf]
+
+
+class FieldSectionEncoder:
+    """Whole field sections out of one qh_encode_sections_batch call: the
+    count kernels, Huffman iff shorter, the encode kernels over the picked
+    strings, then the representation writer kernel (byte for byte
+    qh_qpack_write_sections)."""
+
+    def __init__(self, device: int = 0, codec: HuffmanBatchCodec | None = None):
+        self.codec = codec or HuffmanBatchCodec(device)
+
+    def encode_sections(self, plain, strs, lines, line_start, prefixes=None):
+        """Host arrays -> (dst uint8, sections SPAN_IN_DTYPE)."""
+        lib = _load()
+        plain = _u8(plain)
+        if plain.size == 0:
+            plain = np.zeros(1, dtype=np.uint8)
+        strs = np.ascontiguousarray(strs, dtype=SPAN_IN_DTYPE)
+        lines = np.ascontiguousarray(lines, dtype=FIELD_LINE_DTYPE)
+        if lines.size == 0:
+            lines = np.zeros(1, dtype=FIELD_LINE_DTYPE)[:0]
+        line_start = np.ascontiguousarray(line_start, dtype=np.uint32)
+        nsec = line_start.size - 1
+        pf = None if prefixes is None else np.ascontiguousarray(prefixes, dtype=PREFIX_DTYPE)
+        sections = np.zeros(max(nsec, 1), dtype=SPAN_IN_DTYPE)
+        need = ctypes.c_uint64(0)
+        dst = np.zeros(64, dtype=np.uint8)
+        for _ in range(2):
+            rv = lib.qh_encode_sections_batch(
+                self.codec._ctx, _vp(plain), _vp(strs), strs.size, _vp(lines), _vp(line_start),
+                nsec, None if pf is None else _vp(pf), _vp(dst), dst.size, _vp(sections),
+                ctypes.byref(need), _lib.QH_WHERE_HOST)
+            if rv == _lib.QH_ERR_NOMEM and need.value > dst.size:
+                dst = np.zeros(int(need.value), dtype=np.uint8)
+                continue
+            _lib.check(rv, "qh_encode_sections_batch")
+            break
+        return dst[:need.value], sections[:nsec]
+
+    def encode_sections_dev(self, plain, strs, lines, line_start, dst, sections, prefixes=None):
+        """Device-resident form over torch tensors (plain uint8, strs int64
+        [n,2], lines uint8 [nlines*24], line_start int32 [nsec+1], dst uint8,
+        sections int64 [nsec,2], prefixes optional).  Returns dst_need;
+        raises on QH_ERR_NOMEM."""
+        lib = _load()
+        p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+        need = ctypes.c_uint64(0)
+        rv = lib.qh_encode_sections_batch(self.codec._ctx, p(plain), p(strs), strs.shape[0], p(lines),
+                                          p(line_start), line_start.shape[0] - 1, p(prefixes), p(dst),
+                                          dst.numel(), p(sections), ctypes.byref(need),
+                                          _lib.QH_WHERE_DEVICE)
+        _lib.check(rv, "qh_encode_sections_batch")
+        return need.value
