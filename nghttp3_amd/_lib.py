@@ -134,6 +134,14 @@ def load():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make` or "
             "`python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch's copy when PyTorch is present
+    # (libqhuff's libamdhip64.so.7 then binds to the one torch loaded).
+    # Loading the system runtime first and torch's after leaves two HSA
+    # runtimes in the process, and the device is then invisible to one.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     c = ctypes
     vp, sz, u64, u32, i32 = c.c_void_p, c.c_size_t, c.c_uint64, c.c_uint32, c.c_int

@@ -27,8 +27,8 @@ CORPUS = os.path.join(GOLDEN, "netbsd-hq.out.256.100.1")
 
 
 @pytest.fixture(scope="module")
-def enc():
-    return qpack.FieldSectionEncoder(device=0)
+def enc(codec):
+    return qpack.FieldSectionEncoder(codec=codec)
 
 
 def test_encode_sections_matches_host_writer(enc):
