@@ -293,8 +293,14 @@ def main():
         sp5, tot5 = codec.spans_to_device(ln5[c0:c1])
         src5 = codec.synth_fill(SEED5, f5, tot5, synth.ALPHABET_A)
         enc5, eout5, eb5, dec5, dout5 = buffers(src5, sp5)
+        # skewed lengths: the wave decoder (QH_DECODER_WAVES); the window
+        # decoder's time on the same batch is reported beside it
+        td5_win = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 3)
+        ok5_win = roundtrip_ok(src5, sp5, dec5, dout5)
+        codec.set_decoder("waves")
+        dec5.zero_()
         codec.decode_dev(enc5, eout5, dec5, dout5)
-        ok5 = roundtrip_ok(src5, sp5, dec5, dout5)
+        ok5 = roundtrip_ok(src5, sp5, dec5, dout5) and ok5_win
         te5 = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 5)
         td5 = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 5)
         codec.enable_timing(True)
@@ -302,6 +308,7 @@ def main():
             codec.decode_dev(enc5, eout5, dec5, dout5)
         k5 = kernel_table(codec.kernel_times(), sp5.shape[0], tot5, eb5)
         codec.enable_timing(False)
+        codec.set_decoder("windows")
         d5 = k5.get("qh_k_dec_peek", {})
         p5, e5 = D.sum(float(tot5)), D.sum(float(eb5))
         dec_gbps_min = D.max(-d5.get("achieved_GBps", 0.0))
@@ -310,6 +317,8 @@ def main():
                               "mean %.1f B" % float(ln5.mean()),
                    "shards": world, "strings_rank0": int(c1 - c0) if rank == 0 else None,
                    "encode_GiBps": round(p5 / te5 / GIB, 2), "decode_GiBps": round(p5 / td5 / GIB, 2),
+                   "decoder": "waves (qh_k_dec_peekw: per-wave sorted chunks, LDS-ring input)",
+                   "decode_GiBps_window_decoder": round(p5 / D.max(td5_win) / GIB, 2),
                    "round_trip_GiBps": round(p5 / (te5 + td5) / GIB, 2),
                    "decode_kernel_us_rank0": d5.get("avg_us"),
                    "decode_kernel_GBps_min_rank": round(-dec_gbps_min, 1),
@@ -321,6 +330,11 @@ def main():
     config4 = None
     if not args.no_configs and args.c4_blocks:
         config4 = leg_config4(args, torch, dev, codec, D, rank, world, timed)
+
+    # ---- config 1: the QIF driver on the 1,024-field QIF (rank 0, N = 1) ----
+    config1 = None
+    if rank == 0 and world == 1 and not args.no_configs:
+        config1 = leg_config1()
 
     # ---- alphabet U (config 3 shape), rank 0 alone ----
     configU = None
@@ -376,6 +390,7 @@ def main():
                       "enc_global_offset_rank0": enc_global_off,
                       "kernels": kern, "host_path": host_path,
                       "config5_zipf": config5, "config4_qpack_blocks": config4,
+                      "config1_qif": config1,
                       "config3_alphabet_U": configU},
         }
         print(json.dumps(line), flush=True)
@@ -434,6 +449,27 @@ def leg_config4(args, torch, dev, codec, D, rank, world, timed):
         ok = bool(torch.equal(got, want))
         del starts, pos, at, from_dst, got, want
     valid = int(bufs["verdict"][:ns].to(torch.int64).sum().item())
+    # encoder side: this rank's sections written back from their lines and
+    # plaintext strings (qh_encode_sections_batch on the device)
+    fse = qp.FieldSectionEncoder(codec=codec)
+    e_plain = torch.from_numpy(np.ascontiguousarray(q_plain)).to(dev)
+    e_strs = torch.from_numpy(q_strs.view(np.int64).reshape(-1, 2).copy()).to(dev)
+    l0, l1 = int(q_ls[lo]), int(q_ls[hi])
+    e_lines = torch.from_numpy(np.ascontiguousarray(q_lines[l0:l1]).view(np.uint8).copy()).to(dev)
+    e_ls = torch.from_numpy((q_ls[lo:hi + 1] - q_ls[lo]).astype(np.int32)).to(dev)
+    e_dst = torch.empty(q_host.size + 64, dtype=torch.uint8, device=dev)
+    e_sec = torch.empty((hi - lo, 2), dtype=torch.int64, device=dev)
+    need = fse.encode_sections_dev(e_plain, e_strs, e_lines, e_ls, e_dst, e_sec)
+    torch.cuda.synchronize()
+    enc_ok = need == q_host.size and bool(torch.equal(e_dst[:need], d_src))
+    t_enc = timed(lambda: fse.encode_sections_dev(e_plain, e_strs, e_lines, e_ls, e_dst, e_sec),
+                  args.steps)
+    codec.enable_timing(True)
+    for _ in range(3):
+        fse.encode_sections_dev(e_plain, e_strs, e_lines, e_ls, e_dst, e_sec)
+    kt_enc = {k: round(ms / max(c, 1) * 1e3, 2) for k, (c, ms) in codec.kernel_times().items()}
+    codec.enable_timing(False)
+    del e_plain, e_strs, e_lines, e_ls, e_dst, e_sec
     # host-memory form (the library stages H2D / D2H): this rank's blocks
     reps = 3
     fsd.decode_blocks(q_host, my)
@@ -455,11 +491,48 @@ def leg_config4(args, torch, dev, codec, D, rank, world, timed):
             "host_path_ms": round(t_host * 1e3, 3),
             "host_path_blocks_per_s": round(nb_all / t_host, 1),
             "bit_exact": D.sum(0.0 if ok else 1.0) == 0,
+            "encoder_gpu_ms": round(t_enc * 1e3, 4),
+            "encoder_gpu_blocks_per_s": round(nb_all / t_enc, 1),
+            "encoder_gpu_string_GiBps": round(s_all / t_enc / GIB, 2),
+            "encoder_kernel_avg_us_rank0": kt_enc,
+            "encoder_bit_exact": D.sum(0.0 if enc_ok else 1.0) == 0,
+            "encoder_pipeline": "qh_encode_sections_batch: count -> pick (Huffman iff shorter) -> "
+                                "section sizes -> scan -> (sync) -> encode picked strings -> write",
             "pipeline": "qh_decode_sections_batch: frame count -> scans -> (sync) -> frame write -> "
                         "decode -> post (fold -401, check, tokens)",
             "shape": "synthetic (nghttp3_amd/qpack.py synth_field_sections): 4-20 lines per "
                      "block, 30% indexed static, 40% static name ref, 30% literal name; "
                      "names 4-24 B, values 1-128 B, alphabet A; dtable 0"}
+
+
+def leg_config1():
+    """Config 1: the driver (nghttp3_amd/lib/qpack, a child process) encodes
+    the 1,024-field QIF and decodes it back, on the GPU batch path and on the
+    scalar drop-ins; each batch part timed over 20 repetitions (median), the
+    round trip checked byte for byte."""
+    import tempfile
+    from nghttp3_amd import qif
+    text = qif.synth_config1()
+    res = {"fields": 1024, "qif_bytes": len(text),
+           "source": "nghttp3_amd/qif.py synth_config1 (netbsd QIF, :path queries, cookies; seed 0x5EED0001)"}
+    with tempfile.TemporaryDirectory() as d:
+        src, wire, back = (os.path.join(d, x) for x in ("c1.qif", "c1.out", "c1.back"))
+        open(src, "wb").write(text)
+        for path in ("gpu", "scalar"):
+            flag = [] if path == "gpu" else ["--scalar"]
+            r1 = qif.run(flag + ["--time", "20", "encode", src, wire])
+            r2 = qif.run(flag + ["--time", "20", "decode", wire, back])
+            if r1.returncode or r2.returncode:
+                res[path] = {"error": (r1.stderr + r2.stderr)[-400:]}
+                continue
+            je = json.loads(r1.stderr.strip().splitlines()[-1])
+            jd = json.loads(r2.stderr.strip().splitlines()[-1])
+            ok = open(back, "rb").read() == text
+            res[path] = {"encode_batch_ms": je["batch_ms"], "encode_plan_ms": je["plan_ms"],
+                         "decode_frame_ms": jd["frame_ms"], "decode_batch_ms": jd["batch_ms"],
+                         "decode_replay_ms": jd["replay_ms"], "wire_bytes": je["out_bytes"],
+                         "round_trip_identical": ok}
+    return res
 
 
 def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n):

@@ -24,7 +24,7 @@ QH_ERR_NOMEM = -901
 QH_WHERE_HOST = 0
 QH_WHERE_DEVICE = 1
 QH_DECODER_WINDOWS = 0
-QH_DECODER_QUEUE = 1
+QH_DECODER_WAVES = 1
 
 NGHTTP3_QPACK_HUFFMAN_FLAG_ACCEPTED = 0x01
 NGHTTP3_QPACK_HUFFMAN_FLAG_SYM = 0x02

@@ -8,7 +8,8 @@
 // Shipped kernels (all launched on the context's stream):
 //   qh_k_dec_reserve + qh_k_dec_peek   decode, sorted 256-string windows, a
 //                      W-bit table lookup per code (huffman.c:87-124)
-//   qh_k_dec_wres + qh_k_dec_q         decode, per-wave string queues
+//   qh_k_dec_reserve + qh_k_dec_peekw  decode, per-wave sorted chunks, input
+//                      through LDS rings (QH_DECODER_WAVES)
 //   qh_k_enc_lens_stream / _lane       encoded lengths (huffman.c:34-43)
 //   qh_k_enc_lanes     codes, one string per lane, dense output through an
 //                      LDS stage (huffman.c:45-78)
@@ -16,8 +17,9 @@
 //   qh_k_lookup_tokens QPACK framing, validation and tokens
 //   qh_k_encsec_*      representation writer of whole field sections
 //   qh_k_scan, qh_k_synth_*   prefix sums, synthetic inputs (bench/tests)
-// Development variants (decoders fsm / fsm2 / lut / run / other peek
-// widths, the chunk-engine and streaming encoders) build only with
+// Development variants (decoders fsm / fsm2 / lut / run / queue / other
+// peek widths and shapes, the chunk-engine and streaming encoders) build
+// only with
 // -DQH_DEV_VARIANTS (make dev -> libqhuff_dev.so).
 
 #include <hip/hip_runtime.h>
@@ -50,7 +52,9 @@
 #ifdef QH_DEV_VARIANTS
 #include "qh_dec3.inc"       // decoder: plan + task-queue lanes
 #endif
-#include "qh_dec_q.inc"      // decoder: per-wave string queues (QH_DECODER_QUEUE)
+#ifdef QH_DEV_VARIANTS
+#include "qh_dec_q.inc"      // decoder: per-wave string queues
+#endif
 #include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes)
 #ifdef QH_DEV_VARIANTS
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds

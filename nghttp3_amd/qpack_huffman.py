@@ -168,9 +168,9 @@ class HuffmanBatchCodec:
 
     # -- context utilities --------------------------------------------------
     def set_decoder(self, kind: str):
-        """'windows' (default: strings of similar length) or 'queue' (skewed
+        """'windows' (default: strings of similar length) or 'waves' (skewed
         lengths, e.g. Zipf up to 4 KiB); results are identical."""
-        k = {"windows": _lib.QH_DECODER_WINDOWS, "queue": _lib.QH_DECODER_QUEUE}[kind]
+        k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES}[kind]
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
 
     def sync(self):

@@ -215,8 +215,8 @@ def test_synth_device_matches_host(codec):
 
 
 @pytest.mark.parametrize("name,decoder", [("c2_A", "windows"), ("c2_U", "windows"),
-                                          ("c3_A", "windows"), ("c3_A", "queue"),
-                                          ("c2_U", "queue")])
+                                          ("c3_A", "windows"), ("c3_A", "waves"),
+                                          ("c2_U", "waves")])
 def test_full_size_config(codec, digests, name, decoder):
     """BASELINE configs at full size (2^20 strings): synth digest, encode
     digest vs the oracle's, then decode round trip (size-independent), with
@@ -265,7 +265,7 @@ def _full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
-@pytest.mark.parametrize("decoder", ["windows", "queue"])
+@pytest.mark.parametrize("decoder", ["windows", "waves"])
 def test_config5_rank_shard_full_size(codec, digests, decoder):
     """Config 5 at size: rank 0's shard of 16M Zipf strings split by bytes
     over 8 GPUs (2.1M strings, 438 MB, lengths 1..4096), as bench.py cuts
@@ -430,7 +430,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
 
 # The two shipped decoders (qh_ctx_set_decoder); the development variants
 # (make dev) are timed by scripts/dec_variants.py, not shipped.
-DECODERS = ["windows", "queue"]
+DECODERS = ["windows", "waves"]
 
 
 def codec_of(kind):
@@ -443,7 +443,8 @@ def codec_of(kind):
 @pytest.mark.parametrize("kind", DECODERS)
 def test_decoder_variants(kind, corpus, errors, kat, codec):
     """Both decoders (the window decoder: sorted 256-string windows, W-bit
-    peek table in lock-step; the queue decoder: per-wave string queues)
+    peek table in lock-step; the wave decoder: per-wave sorted chunks, input
+    through LDS rings)
     give the oracle's bytes and statuses: golden corpus, corrupted strings,
     the reference's error verdicts, RFC vectors, and mixed lengths 0-5000 B
     over alphabet A and all 256 byte values (long codes, EOS-prefix ends)."""
