@@ -180,7 +180,12 @@ QH_EXPORT int qh_ctx_last_stats(qh_ctx *ctx, qh_batch_stats *stats);
  * of the slots is what a batch needs; out[i].off is the start of the slot
  * and out[i].len the decoded length.  The other bytes of a slot are
  * unspecified.  A string whose slot does not fit in dst_cap gets
- * QH_ERR_NOMEM; nothing is written at or past dst_cap.
+ * QH_ERR_NOMEM; nothing is written at or past dst_cap.  With QH_WHERE_HOST
+ * the decoded strings come back packed: dst holds them back to back and
+ * out[i].off = the sum of the decoded lengths before string i (only decoded
+ * bytes cross PCIe; the batch is pipelined in slices over copy and compute
+ * streams); dst_cap >= qh_decode_dst_size(in, n) still always suffices, and a
+ * string whose bytes would pass dst_cap gets QH_ERR_NOMEM.
  * Encode output is dense: out[i].off = sum_{j<i} encode_count(string j);
  * qh_encode_dst_bound() is an upper bound. */
 QH_EXPORT uint64_t qh_decode_dst_size(const qh_span_in *in, size_t n);

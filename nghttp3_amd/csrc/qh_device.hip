@@ -60,6 +60,7 @@
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
 #endif
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
+#include "qh_host.inc"   // host-memory decode: dense packing kernels
 #include "qh_api.inc"    // host API (include/qhuff.h)
 #include "qh_validate.inc"  // field name / value validation batch, header-name tokens
 #include "qh_frame.inc"     // QPACK field-section framing on the device

@@ -204,6 +204,49 @@ def test_host_path_matches(codec, corpus):
     assert (codec.encode_count_host(plain, psp) == corpus["enc_len"]).all()
 
 
+def test_host_path_full_size_packed_and_pipelined(codec, digests):
+    """Host-memory decode of config 3 at size (2^20 strings: eight slices on
+    the copy / compute streams): out[i].off is the packed offset, and the
+    packed bytes are the plaintext; with a dst_cap of half the plaintext
+    the strings past it get QH_ERR_NOMEM and the rest still decode."""
+    torch = torch_mod()
+    d = digests["c3_A"]
+    src, spans, total = codec.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_A)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    e_h = enc[:d["enc_bytes"]].cpu().numpy()
+    eo = eout.cpu().numpy()
+    sp = np.zeros(d["n"], dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    plain = src[:total].cpu().numpy()
+    lens = (spans[:, 1] & 0xFFFFFFFF).cpu().numpy()
+    dst, out = codec.decode_host(e_h, sp)
+    assert (out["status"] == 0).all() and (out["len"] == lens).all()
+    assert (out["off"][1:] == np.cumsum(lens)[:-1]).all() and out["off"][0] == 0
+    assert dst[:total].tobytes() == plain.tobytes()
+    st = codec.stats()
+    assert st["n_errors"] == 0 and st["out_bytes"] == total
+    half = total // 2
+    small = np.zeros(half, dtype=np.uint8)
+    out2 = np.zeros(d["n"], dtype=q.SPAN_OUT_DTYPE)
+    import ctypes
+    from nghttp3_amd import _lib
+    rv = codec._lib.qh_decode_batch(codec._ctx, e_h.ctypes.data_as(ctypes.c_void_p),
+                                    sp.ctypes.data_as(ctypes.c_void_p), d["n"],
+                                    small.ctypes.data_as(ctypes.c_void_p), half,
+                                    out2.ctypes.data_as(ctypes.c_void_p), _lib.QH_WHERE_HOST)
+    assert rv == 0
+    ok = out2["status"] == 0
+    assert set(np.unique(out2["status"])) <= {0, q.QH_ERR_NOMEM} and ok.any() and (~ok).any()
+    k = int(np.argmin(ok))  # the first string that did not fit; none after it fits
+    assert ok[:k].all() and not ok[k:].any()
+    end = int(out2["off"][k - 1] + out2["len"][k - 1])
+    assert end <= half and small[:end].tobytes() == plain[:end].tobytes()
+
+
 def test_synth_device_matches_host(codec):
     src, spans, total = codec.synth(0x1234, 5000, 1, 300, synth.ALPHABET_A)
     plain, off, ln = synth.batch(0x1234, 5000, 1, 300, synth.ALPHABET_A)
