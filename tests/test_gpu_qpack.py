@@ -319,3 +319,13 @@ def test_gpu_framing_matches_host_scan_on_netbsd_and_synthetic(dec):
     _same_scan(_gpu_scan(dec, src, blocks), qpack.scan_blocks(src, blocks))
     st = _gpu_scan(dec, src, blocks)[4]
     assert (st[[11, 12]] == qpack.QH_ERR_QPACK_DECOMPRESSION_FAILED).all() and (st[:10] == 0).all()
+    # blocks larger than the count pass's per-block slice (32 lines / 64
+    # strings) are parsed again in the write pass: mixed with small ones
+    src, blocks, *_ = qpack.synth_field_sections(0x5EED000A, 600, fields=(1, 120))
+    src = src.copy()
+    blocks = blocks.copy()
+    blocks["len"][7] -= 1  # a big block that fails
+    got = _gpu_scan(dec, src, blocks)
+    _same_scan(got, qpack.scan_blocks(src, blocks))
+    nl = np.diff(got[2].astype(np.int64))
+    assert (nl > 32).sum() > 100 and (nl <= 32).sum() > 100
