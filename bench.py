@@ -301,6 +301,15 @@ def main():
         dec5.zero_()
         codec.decode_dev(enc5, eout5, dec5, dout5)
         ok5 = roundtrip_ok(src5, sp5, dec5, dout5) and ok5_win
+        # and the wave encoder (QH_ENCODER_WAVES): its bytes must be the
+        # window encoder's; the window encoder's time is reported beside it
+        te5_win = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 3)
+        enc5_win, eout5_win = enc5[:eb5].clone(), eout5.clone()
+        codec.set_encoder("waves")
+        enc5.zero_()
+        codec.encode_dev(src5, sp5, enc5, eout5)
+        ok5 = ok5 and bool(torch.equal(enc5[:eb5], enc5_win)) and bool(torch.equal(eout5, eout5_win))
+        del enc5_win, eout5_win
         te5 = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 5)
         td5 = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 5)
         codec.enable_timing(True)
@@ -309,6 +318,7 @@ def main():
         k5 = kernel_table(codec.kernel_times(), sp5.shape[0], tot5, eb5)
         codec.enable_timing(False)
         codec.set_decoder("windows")
+        codec.set_encoder("windows")
         d5 = k5.get("qh_k_dec_peek", {})
         p5, e5 = D.sum(float(tot5)), D.sum(float(eb5))
         dec_gbps_min = D.max(-d5.get("achieved_GBps", 0.0))
@@ -319,6 +329,8 @@ def main():
                    "encode_GiBps": round(p5 / te5 / GIB, 2), "decode_GiBps": round(p5 / td5 / GIB, 2),
                    "decoder": "waves (qh_k_dec_peekw: per-wave sorted chunks, LDS-ring input)",
                    "decode_GiBps_window_decoder": round(p5 / D.max(td5_win) / GIB, 2),
+                   "encoder": "waves (qh_k_enc_waves: per-wave sorted chunks, LDS-ring output)",
+                   "encode_GiBps_window_encoder": round(p5 / D.max(te5_win) / GIB, 2),
                    "round_trip_GiBps": round(p5 / (te5 + td5) / GIB, 2),
                    "decode_kernel_us_rank0": d5.get("avg_us"),
                    "decode_kernel_GBps_min_rank": round(-dec_gbps_min, 1),

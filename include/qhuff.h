@@ -165,6 +165,16 @@ QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
 #define QH_DECODER_WINDOWS 0
 #define QH_DECODER_WAVES 1
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
+/* Codes kernel of qh_encode_batch (results are identical; speed is not):
+ * QH_ENCODER_WINDOWS (default) encodes a sorted window of up to 256 strings
+ * per workgroup into an LDS stage copied out with coalesced stores --
+ * fastest for strings of similar length; QH_ENCODER_WAVES lets every wave
+ * sort and encode its own chunks of 256 strings with no workgroup barrier,
+ * each lane writing its string's 16-byte output chunks from an LDS ring --
+ * fastest for skewed or long strings (Zipf up to 4 KiB: 2.3x). */
+#define QH_ENCODER_WINDOWS 0
+#define QH_ENCODER_WAVES 1
+QH_EXPORT int qh_ctx_set_encoder(qh_ctx *ctx, int kind);
 QH_EXPORT void *qh_ctx_stream(qh_ctx *ctx);
 /* Wait for all work queued on the context's stream. */
 QH_EXPORT int qh_ctx_sync(qh_ctx *ctx);

@@ -25,6 +25,8 @@ QH_WHERE_HOST = 0
 QH_WHERE_DEVICE = 1
 QH_DECODER_WINDOWS = 0
 QH_DECODER_WAVES = 1
+QH_ENCODER_WINDOWS = 0
+QH_ENCODER_WAVES = 1
 
 NGHTTP3_QPACK_HUFFMAN_FLAG_ACCEPTED = 0x01
 NGHTTP3_QPACK_HUFFMAN_FLAG_SYM = 0x02
@@ -83,6 +85,7 @@ EXPORTED_FUNCTIONS = (
     "qh_ctx_del",
     "qh_ctx_set_stream",
     "qh_ctx_set_decoder",
+    "qh_ctx_set_encoder",
     "qh_ctx_stream",
     "qh_ctx_sync",
     "qh_ctx_last_stats",
@@ -164,6 +167,8 @@ def load():
     lib.qh_ctx_del.restype = None
     lib.qh_ctx_set_decoder.argtypes = [vp, i32]
     lib.qh_ctx_set_decoder.restype = i32
+    lib.qh_ctx_set_encoder.argtypes = [vp, i32]
+    lib.qh_ctx_set_encoder.restype = i32
     lib.qh_ctx_set_stream.argtypes = [vp, vp]
     lib.qh_ctx_set_stream.restype = i32
     lib.qh_ctx_stream.argtypes = [vp]

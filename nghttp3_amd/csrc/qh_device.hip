@@ -57,6 +57,7 @@
 #include "qh_dec_q.inc"      // decoder: per-wave string queues
 #endif
 #include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes)
+#include "qh_enc_waves.inc"   // encoder codes (default): per-wave chunks, LDS rings
 #ifdef QH_DEV_VARIANTS
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
 #endif

@@ -173,6 +173,12 @@ class HuffmanBatchCodec:
         k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES}[kind]
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
 
+    def set_encoder(self, kind: str):
+        """'windows' (default: strings of similar length) or 'waves' (skewed
+        or long strings); results are identical."""
+        k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES}[kind]
+        _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")
+
     def sync(self):
         _lib.check(self._lib.qh_ctx_sync(self._ctx), "qh_ctx_sync")
 

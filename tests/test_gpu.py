@@ -265,10 +265,12 @@ def test_full_size_config(codec, digests, name, decoder):
     digest vs the oracle's, then decode round trip (size-independent), with
     either shipped decoder."""
     codec.set_decoder(decoder)
+    codec.set_encoder(decoder)
     try:
         _full_size_config(codec, digests, name)
     finally:
         codec.set_decoder("windows")
+        codec.set_encoder("windows")
 
 
 def _full_size_config(codec, digests, name):
@@ -315,10 +317,12 @@ def test_config5_rank_shard_full_size(codec, digests, decoder):
     it: the device generator from the global byte offset, encode digests vs
     the oracle's, then the decode round trip (chunked compare)."""
     codec.set_decoder(decoder)
+    codec.set_encoder(decoder)  # the shipped kernel pair for skewed lengths
     try:
         _config5_rank_shard(codec, digests)
     finally:
         codec.set_decoder("windows")
+        codec.set_encoder("windows")
 
 
 def _config5_rank_shard(codec, digests):
@@ -611,3 +615,61 @@ def test_zipf_lengths_roundtrip(codec, alphabet):
     assert (ds == 0).all() and (dl == ln).all()
     for j in range(0, n, 37):
         assert dst[do[j]:do[j] + dl[j]].tobytes() == plain[off[j]:off[j] + ln[j]].tobytes(), j
+
+
+# The two shipped encoders (qh_ctx_set_encoder): the window encoder (a
+# sorted 256-string window per workgroup, LDS stage, coalesced copy-out) and
+# the wave encoder (per-wave sorted chunks, LDS rings, per-lane 16-byte
+# output chunks).
+ENCODERS = ["windows", "waves"]
+
+
+@pytest.mark.parametrize("kind", ENCODERS)
+def test_encoder_variants(kind, corpus, kat, digests):
+    """Both encoders give the oracle's bytes: RFC vectors, the golden corpus,
+    unordered / gapped / overlapping spans, mixed lengths 0-40000 B over
+    alphabet A and all 256 byte values, Zipf lengths, dst_cap refusals, an
+    output buffer at every alignment mod 16, and the full-size c2_U digest."""
+    from nghttp3_amd import HuffmanBatchCodec
+    torch = torch_mod()
+    c = HuffmanBatchCodec(device=0)
+    c.set_encoder(kind)
+    try:
+        plains = [v["plain"].encode() for v in kat]
+        src, sp = q.pack_strings(plains)
+        enc, o, l, s = encode_dev(c, src, sp["off"], sp["len"])
+        for i, v in enumerate(kat):
+            assert enc[o[i]:o[i] + l[i]].tobytes().hex() == v["huffman_hex"]
+        test_corpus_encode(c, corpus)
+        test_encode_unordered_spans(c, corpus)
+        test_encode_gapped_spans(c, corpus)
+        test_encode_overlapping_spans(c, corpus)
+        test_mixed_lengths_roundtrip(c)
+        test_encode_dst_cap_too_small(c, corpus)
+        test_zipf_lengths_roundtrip(c, "U")
+        # dst at every alignment: strings' first / last output chunks are
+        # written bytewise where they share a dword with a neighbour
+        plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+        n = 2000
+        want_len = corpus["enc_len"][:n].astype(np.int64)
+        total = int(want_len.sum())
+        srcd, spd = to_dev(plain), spans_dev(off[:n], ln[:n])
+        for a in range(16):
+            buf = torch.full((total + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+            out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+            c.encode_dev(srcd, spd, buf[a:a + total], out)
+            d = buf.cpu().numpy()
+            assert (d[:a] == 0x5A).all() and (d[a + total:] == 0x5A).all(), a
+            assert (d[a:a + total] == corpus["enc"][:total]).all(), a
+        d = digests["c2_U"]
+        srcu, spans, _ = c.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_U)
+        lnu = spans[:, 1] & 0xFFFFFFFF
+        encu = torch.zeros(int(((lnu * 30 + 7) // 8).sum().item()), dtype=torch.uint8,
+                           device="cuda")
+        eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+        c.encode_dev(srcu, spans, encu, eout)
+        st = c.stats()
+        assert st["n_errors"] == 0 and st["out_bytes"] == d["enc_bytes"]
+        assert sha(encu[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
+    finally:
+        c.close()
