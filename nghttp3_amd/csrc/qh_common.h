@@ -39,6 +39,12 @@ struct StampAcc {
   }
   __device__ void count(int k, unsigned long long v) { a[k] += v; }
   __device__ void wait_mem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+  // slots 0..6 and 11 only (a helper's own phases), from thread 0
+  __device__ void add_slots() {
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 12; ++k)
+        if (a[k] && (k < 7 || k == 11)) atomicAdd(&g_stamps[k], a[k]);
+  }
   __device__ void flush() {  // slots 12, 13: block lifetime in realtime (100 MHz) / memtime
     const unsigned long long life = __builtin_amdgcn_s_memrealtime() - r0;
     a[12] += life;
@@ -66,6 +72,7 @@ struct StampAcc {
   __device__ void st(int) {}
   __device__ void count(int, unsigned long long) {}
   __device__ void wait_mem() {}
+  __device__ void add_slots() {}
   __device__ void flush() {}
 };
 #define QH_ST_INIT()

@@ -13,12 +13,13 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nghttp3_amd import HuffmanBatchCodec, _lib  # noqa: E402
 from nghttp3_amd.qpack_huffman import decode_slot_size  # noqa: E402
-from nghttp3_amd.synth import ALPHABET_A  # noqa: E402
+from nghttp3_amd.synth import ALPHABET_A, ALPHABET_U  # noqa: E402
 
 # kernel -> (phase slots, rounds slot, tiles slot, extra counter slot)
 LAYOUT = {
     "dec_lanes": ({0: "window", 1: "decode"}, 10, 10, None),
-    "dec_peek": ({0: "window", 4: "start", 3: "top wait", 2: "body", 1: "end"}, 11, 10, None),
+    "dec_peek": ({0: "window setup", 1: "window decode (all)", 2: "str start", 3: "iter top",
+                  4: "iter body", 5: "careful", 6: "str end"}, 11, 10, None),
     "enc_lens": ({0: "head", 2: "dma wait", 3: "lookups", 4: "scan", 5: "ends", 6: "tail"},
                  10, 10, 11),
     "enc_lanes": ({0: "head", 1: "wait+zero", 2: "bits+scan", 3: "starts", 4: "emit",
@@ -39,7 +40,8 @@ def main():
     n = int(os.environ.get("N", 1 << 20))
     codec = HuffmanBatchCodec(0)
     dev = torch.device("cuda", 0)
-    src, spans, total = codec.synth(0x5EED0003, n, 8, 256, ALPHABET_A)
+    src, spans, total = codec.synth(0x5EED0003, n, 8, 256,
+                                    ALPHABET_U if os.environ.get("ALPH") == "U" else ALPHABET_A)
     enc = torch.empty(total * 4 + 64, dtype=torch.uint8, device=dev)
     eout = torch.empty((n, 2), dtype=torch.int64, device=dev)
     dout = torch.empty((n, 2), dtype=torch.int64, device=dev)

@@ -547,6 +547,67 @@ def test_decoder_variants(kind, corpus, errors, kat, codec):
         c.close()
 
 
+def _long_mode_batch(rng):
+    """Strings that drive the window decoder's long iterations (V & 256):
+    binary text, binary then header text and back, errors met inside long
+    iterations (an EOS code mid-string, a cut last code, bad padding), and
+    header text sharing windows with them."""
+    A = np.frombuffer(synth.ALPHABET_A, dtype=np.uint8)
+    def txt(alpha, n):
+        return bytes(alpha[rng.integers(0, len(alpha), n)]) if alpha is not None else \
+            bytes(rng.integers(0, 256, n).astype(np.uint8))
+    plain = []
+    for i in range(6000):
+        k = i % 6
+        n = int(rng.integers(0, 400))
+        if k == 0:
+            plain.append(txt(None, n))                          # binary
+        elif k == 1:
+            plain.append(txt(None, n) + txt(A, n))              # binary, then text
+        elif k == 2:
+            plain.append(txt(A, n // 4) + txt(None, n) + txt(A, 20))
+        else:
+            plain.append(txt(A, n))                             # text in the same windows
+    encs = [oracle.encode(x) for x in plain]
+    out = []
+    eos = bytes([0xFF, 0xFF, 0xFF, 0xFC])  # 30 ones then 00: an EOS code
+    for i, e in enumerate(encs):
+        k = i % 7
+        if k == 3 and len(e) > 8:
+            j = int(rng.integers(1, len(e) - 4))
+            e = e[:j] + eos + e[j:]                            # EOS mid-string
+        elif k == 4 and len(e) > 1:
+            e = e[:-int(rng.integers(1, min(len(e), 5)))]      # cut inside the last codes
+        elif k == 5 and len(e) > 1:
+            e = e[:-1] + bytes([e[-1] & 0xFE])                 # padding with a zero bit
+        elif k == 6 and len(e) > 2:
+            j = int(rng.integers(0, len(e)))
+            e = e[:j] + bytes([e[j] ^ (1 << int(rng.integers(0, 8)))]) + e[j + 1:]
+        out.append(e)
+    return out
+
+
+@pytest.mark.parametrize("kind", DECODERS)
+def test_long_code_mode_matches_oracle(kind):
+    """Binary-heavy strings (the long-code iterations of the window decoder,
+    the careful path of both) with errors inside them: statuses, lengths and
+    bytes as the oracle's decode of lib/nghttp3_qpack_huffman.c."""
+    c = codec_of(kind)
+    try:
+        strs = _long_mode_batch(np.random.default_rng(4242))
+        src, sp = q.pack_strings(strs)
+        want_dst, want_slot, want_len, want_st = oracle.decode_batch(src, sp["off"], sp["len"])
+        assert (want_st != 0).sum() > 1000 and (want_st == 0).sum() > 3000
+        dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+        assert (s == want_st.astype(np.int64)).all()
+        assert (l == want_len.astype(np.int64)).all()
+        for j in np.nonzero(s == 0)[0]:
+            ws = int(want_slot[j])
+            assert dst[o[j]:o[j] + l[j]].tobytes() == want_dst[ws:ws + int(want_len[j])].tobytes(), j
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("mode", ["default", "lane"])
 def test_encode_length_passes(mode, corpus, digests):
     """The encoder's passes: streaming lengths + lane-per-string codes
