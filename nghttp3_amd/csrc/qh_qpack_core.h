@@ -107,11 +107,13 @@ QH_HD static inline int read_string(scan_out *o, int32_t *span_idx, const uint8_
   if (o->nspans == o->spans_cap) {
     return QH_ERR_NOMEM;
   }
-  if (o->spans) {
+  if (o->spans) { /* one whole-record store (the GPU framing kernel) */
+    qh_span_in rec;
+    rec.off = base_off + (uint64_t)(p - base);
+    rec.len = (uint32_t)len;
+    rec.flags = h | kind;
     s = &o->spans[o->nspans];
-    s->off = base_off + (uint64_t)(p - base);
-    s->len = (uint32_t)len;
-    s->flags = h | kind;
+    *s = rec;
   }
   *span_idx = (int32_t)o->nspans++;
   o->nhuff += h ? 1 : 0;
@@ -182,7 +184,8 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
     uint8_t b = *p, opcode, flags = 0;
     unsigned iprefix;
     int has_name_idx = 1, has_value = 1;
-    qh_field_line *l;
+    qh_field_line cur, *l = &cur; /* built here, stored whole at its end */
+    size_t li;
 
     /* qpack.c:3439-3495 */
     if (b & 0x80u) {
@@ -210,10 +213,18 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
       flags = (uint8_t)(QH_FL_DYNAMIC | ((b & 0x08u) ? QH_FL_NEVER : 0));
       iprefix = 3;
     }
-    l = new_line(o, opcode, flags);
-    if (l == NULL) {
+    if (o->nlines == o->lines_cap) {
       return QH_ERR_NOMEM;
     }
+    li = o->nlines++; /* (a line cut short by an error is never stored: the
+                          callers drop a failed block's lines) */
+    cur.index = 0;
+    cur.reserved = 0;
+    cur.reserved2 = 0;
+    cur.opcode = opcode;
+    cur.flags = flags;
+    cur.name = -1;
+    cur.value = -1;
     if (has_name_idx) {
       rv = read_varint(&l->index, &p, end, iprefix);
       if (rv <= 0) {
@@ -243,6 +254,9 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
       if (rv <= 0) {
         return rv < 0 ? rv : bad;
       }
+    }
+    if (o->lines) {
+      o->lines[li] = cur;
     }
   }
   return 0;
