@@ -49,15 +49,15 @@
 #include "qh_lane_dec2.inc"  // decoder: 4-bit FSM, two strings per lane
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #endif
-#include "qh_peek_dec.inc"   // decoder (default): W-bit peek table, sorted windows
+#include "qh_peek_dec.inc"   // decoders (windows: default; waves): W-bit peek table + leading-ones table
 #ifdef QH_DEV_VARIANTS
 #include "qh_dec3.inc"       // decoder: plan + task-queue lanes
 #endif
 #ifdef QH_DEV_VARIANTS
 #include "qh_dec_q.inc"      // decoder: per-wave string queues
 #endif
-#include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes)
-#include "qh_enc_waves.inc"   // encoder codes (default): per-wave chunks, LDS rings
+#include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes: the default)
+#include "qh_enc_waves.inc"   // encoder codes (QH_ENCODER_WAVES): per-wave chunks, LDS rings
 #ifdef QH_DEV_VARIANTS
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
 #endif
