@@ -31,6 +31,7 @@
 
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/qhuff.h"

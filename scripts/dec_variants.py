@@ -2,7 +2,7 @@
 """Time every decoder variant (QHUFF_DECODER) on a BASELINE-shaped batch and
 check each against the plaintext (development tool, one GPU).  Loads the
 development build (make dev -> nghttp3_amd/lib/libqhuff_dev.so), which holds
-every variant; the product library ships peek11u and wring11x16r2 only.
+every variant; the product library ships peek11s and wring11x16r2 only.
 
 Usage: python scripts/dec_variants.py [--n N] [--alphabet A|U] [--reps R]
          [--kinds fsm,peek11,...]
@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--hi", type=int, default=256)
     ap.add_argument("--alphabet", default="A")
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--kinds", default="wring11x16r2,peek11u")
+    ap.add_argument("--kinds", default="wring11x16r2,peek11s")
     ap.add_argument("--zipf", action="store_true", help="config 5 lengths (Zipf 1..4096)")
     args = ap.parse_args()
     import torch
