@@ -3,6 +3,8 @@ qh_encode_batch through the C ABI) against the oracle and the committed
 fixtures.  Integer/byte work, so every comparison is bit-exact."""
 import hashlib
 
+import os
+
 import numpy as np
 import pytest
 
@@ -478,10 +480,23 @@ def test_encode_dst_cap_too_small(codec, corpus):
 # The two shipped decoders (qh_ctx_set_decoder); the development variants
 # (make dev) are timed by scripts/dec_variants.py, not shipped.
 DECODERS = ["windows", "waves"]
+# (development: QHUFF_LIB=nghttp3_amd/lib/libqhuff_dev.so QH_TEST_DEV_DECODERS=
+# peek11su,... adds those variants of the development build to these tests)
+DECODERS += ["dev:" + k for k in os.environ.get("QH_TEST_DEV_DECODERS", "").split(",") if k]
 
 
 def codec_of(kind):
     from nghttp3_amd import HuffmanBatchCodec
+    if kind.startswith("dev:"):
+        old = os.environ.get("QHUFF_DECODER")
+        os.environ["QHUFF_DECODER"] = kind[4:]
+        try:
+            return HuffmanBatchCodec(device=0)
+        finally:
+            if old is None:
+                del os.environ["QHUFF_DECODER"]
+            else:
+                os.environ["QHUFF_DECODER"] = old
     c = HuffmanBatchCodec(device=0)
     c.set_decoder(kind)
     return c
