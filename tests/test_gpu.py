@@ -111,6 +111,41 @@ def test_corpus_encode(codec, corpus):
     assert (enc[:total] == corpus["enc"]).all()
 
 
+def test_stats_describe_the_last_op(corpus):
+    """qh_ctx_last_stats after each op of a sequence on one context reports
+    that op alone: the stats are double-buffered and an op's first kernel
+    zeroes the buffer the next op uses (no memset command), so nothing of an
+    earlier op may leak into a later one, in any order of ops."""
+    from nghttp3_amd import HuffmanBatchCodec
+    c = HuffmanBatchCodec(device=0)
+    try:
+        bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+        nbad = int((corpus["bad_status"] != 0).sum())
+        bad_out = int(corpus["bad_out_len"].astype(np.int64)[corpus["bad_status"] == 0].sum())
+        enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+        plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+        ptotal, etotal = int(ln.astype(np.int64).sum()), int(elen.astype(np.int64).sum())
+        for rep in range(3):
+            _, _, _, s = decode_dev(c, bad, boff, blen)
+            st = c.stats()
+            assert st["n"] == len(blen) and st["n_errors"] == nbad and st["out_bytes"] == bad_out, (rep, st)
+            _, _, _, s = encode_dev(c, plain, off, ln)
+            st = c.stats()
+            assert st["n"] == len(ln) and st["n_errors"] == 0 and st["out_bytes"] == etotal, (rep, st)
+            _, _, _, s = decode_dev(c, enc, eoff, elen)
+            st = c.stats()
+            assert st["n"] == len(elen) and st["n_errors"] == 0 and st["out_bytes"] == ptotal, (rep, st)
+            _, _, _, s = decode_dev(c, enc, eoff, elen)  # the same op twice in a row
+            st = c.stats()
+            assert st["n_errors"] == 0 and st["out_bytes"] == ptotal and st["in_bytes"] == etotal, (rep, st)
+            _, _, _, s = encode_dev(c, plain, off, ln)
+            _, _, _, s = encode_dev(c, plain, off, ln)
+            st = c.stats()
+            assert st["n_errors"] == 0 and st["out_bytes"] == etotal, (rep, st)
+    finally:
+        c.close()
+
+
 def test_corpus_encode_count(codec, corpus):
     torch = torch_mod()
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
