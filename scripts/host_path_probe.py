@@ -39,6 +39,28 @@ def main():
         with torch.cuda.stream(s2):
             h2.copy_(d2, non_blocking=True)
     res["both_GBps_each"] = nb / t(both) / 1e9
+    if hasattr(c._lib, "qh_debug_copy16"):  # development build: zero-copy kernel copies
+        import ctypes
+        lib = c._lib
+        lib.qh_debug_copy16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_uint64, ctypes.c_void_p]
+
+        def kcopy(dst, src, st):
+            assert lib.qh_debug_copy16(c._ctx, dst.data_ptr(), src.data_ptr(), nb, st.cuda_stream) == 0
+        res["kernel_d2h_GBps"] = nb / t(lambda: kcopy(h2, d2, s2)) / 1e9
+        res["kernel_h2d_GBps"] = nb / t(lambda: kcopy(d1, h1, s1)) / 1e9
+
+        def sdma_h2d_kernel_d2h():
+            with torch.cuda.stream(s1):
+                d1.copy_(h1, non_blocking=True)
+            kcopy(h2, d2, s2)
+        res["sdma_h2d_with_kernel_d2h_GBps_each"] = nb / t(sdma_h2d_kernel_d2h) / 1e9
+
+        def kernels_both():
+            kcopy(d1, h1, s1)
+            kcopy(h2, d2, s2)
+        res["kernel_both_GBps_each"] = nb / t(kernels_both) / 1e9
+        assert torch.equal(h2[:4096].cpu(), d2[:4096].cpu()) and torch.equal(d1[-4096:].cpu(), h1[-4096:])
     src, spans, total = c.synth(0x5EED0003, 1 << 20, 8, 256, synth.ALPHABET_A)
     ln = spans[:, 1] & 0xFFFFFFFF
     enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")

@@ -284,6 +284,64 @@ def test_host_path_full_size_packed_and_pipelined(codec, digests):
     assert end <= half and small[:end].tobytes() == plain[:end].tobytes()
 
 
+def test_host_path_pinned_buffers(codec, corpus, digests):
+    """Host-memory decode into pinned dst / out (direct DMA; in development
+    builds with QHUFF_HOST_ZC=1 the device-to-host leg as shader stores into
+    the caller's buffers, qh_k_copy16): config 3 at size gives the same
+    packed bytes and spans as the pageable (staged-copy) path and writes
+    nothing past them; a dst_cap of half the plaintext cuts at a string and
+    is respected; the corpus's corrupted strings give the oracle's
+    statuses."""
+    torch = torch_mod()
+    d = digests["c3_A"]
+    src, spans, total = codec.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_A)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    e_h = enc[:d["enc_bytes"]].cpu().numpy()
+    eo = eout.cpu().numpy()
+    sp = np.zeros(d["n"], dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    plain = src[:total].cpu().numpy()
+    cap = int(q.decode_slot_size(sp["len"].astype(np.int64)).sum())
+    pd = torch.full((cap,), 0xAB, dtype=torch.uint8).pin_memory()
+    po = torch.zeros(d["n"] * 2, dtype=torch.int64).pin_memory()
+    dst, out = codec.decode_host(e_h, sp, pd.numpy(), po.numpy().view(q.SPAN_OUT_DTYPE))
+    dst_p, out_p = codec.decode_host(e_h, sp)  # pageable: the staged copies
+    assert (out == out_p).all() and (out["status"] == 0).all()
+    assert dst[:total].tobytes() == plain.tobytes() == dst_p[:total].tobytes()
+    assert (dst[total:] == 0xAB).all()  # nothing written past the packed bytes
+    half = total // 2
+    ph = torch.full((half + 64,), 0xCD, dtype=torch.uint8).pin_memory()
+    po2 = torch.zeros(d["n"] * 2, dtype=torch.int64).pin_memory()
+    out2 = po2.numpy().view(q.SPAN_OUT_DTYPE)
+    import ctypes
+    from nghttp3_amd import _lib
+    rv = codec._lib.qh_decode_batch(codec._ctx, e_h.ctypes.data_as(ctypes.c_void_p),
+                                    sp.ctypes.data_as(ctypes.c_void_p), d["n"],
+                                    ctypes.c_void_p(ph.data_ptr()), half,
+                                    out2.ctypes.data_as(ctypes.c_void_p), _lib.QH_WHERE_HOST)
+    assert rv == 0
+    ok = out2["status"] == 0
+    k = int(np.argmin(ok))
+    assert ok[:k].all() and not ok[k:].any() and k > 0
+    end = int(out2["off"][k - 1] + out2["len"][k - 1])
+    small = ph.numpy()
+    assert end <= half and small[:end].tobytes() == plain[:end].tobytes()
+    assert (small[half:] == 0xCD).all()  # dst_cap is respected
+    bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+    bsp = np.zeros(len(blen), dtype=q.SPAN_IN_DTYPE)
+    bsp["off"], bsp["len"] = boff, blen
+    bcap = int(q.decode_slot_size(blen.astype(np.int64)).sum())
+    pb = torch.zeros(bcap, dtype=torch.uint8).pin_memory()
+    pbo = torch.zeros(len(blen) * 2, dtype=torch.int64).pin_memory()
+    _, bout = codec.decode_host(bad, bsp, pb.numpy(), pbo.numpy().view(q.SPAN_OUT_DTYPE))
+    assert (bout["status"] == corpus["bad_status"]).all()
+    assert (bout["len"] == corpus["bad_out_len"].astype(np.int64)).all()
+
+
 def test_synth_device_matches_host(codec):
     src, spans, total = codec.synth(0x1234, 5000, 1, 300, synth.ALPHABET_A)
     plain, off, ln = synth.batch(0x1234, 5000, 1, 300, synth.ALPHABET_A)
