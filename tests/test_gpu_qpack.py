@@ -174,6 +174,26 @@ def test_sections_pipeline_matches_oracle_on_corrupted_blocks(dec, dec0, refdata
     assert lines.tobytes() == res["lines"].tobytes()
 
 
+@pytest.mark.parametrize("nblocks", [1, 2, 2047, 2048, 2049, 4097])
+def test_sections_pipeline_at_scan_tile_edges(dec0, refdata, nblocks):
+    """Framing's four per-block counts go through one segmented scan launch
+    (qh_k_scan_seg, 2048 entries per tile, one segment per count) whose
+    totals come back in one copy: block counts around the tile size give
+    the oracle's results, host and device forms alike."""
+    import torch
+    src, blocks, kinds = _corrupted_corpus(0x5EED00E0 + nblocks, nblocks)
+    res = dec0.decode_blocks(src, blocks)
+    _check_against_oracle(src, blocks, res, refdata, True)
+    g = dec0.decode_blocks_dev(torch.from_numpy(src).cuda(),
+                               torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+    torch.cuda.synchronize()
+    assert int(g["nspans"]) == res["spans"].size and int(g["nlines"]) == res["lines"].size
+    assert (g["status"][:nblocks].cpu().numpy() == res["status"]).all()
+    assert (g["span_start"][:nblocks + 1].cpu().numpy().view(np.uint32) == res["span_start"]).all()
+    lines = g["lines"][:int(g["nlines"]) * 24].cpu().numpy().view(qpack.FIELD_LINE_DTYPE)
+    assert lines.tobytes() == res["lines"].tobytes()
+
+
 def test_sections_pipeline_clean_blocks_give_the_writer_plaintext(dec0):
     src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED000A, 3000)
     res = dec0.decode_blocks(src, blocks)
