@@ -52,6 +52,17 @@ def test_encode_sections_matches_host_writer(enc):
         assert sec == head + body
 
 
+@pytest.mark.parametrize("nsec", [1, 2047, 2048, 2049, 4097])
+def test_encode_sections_at_scan_tile_edges(enc, nsec):
+    """The section sizes go through one scan launch whose total comes back
+    with the picked-string bytes in one copy (qh_k_scan_seg): section counts
+    around the 2048-entry tile still give the host writer's bytes."""
+    src, blocks, plain, strs, lines, line_start = qpack.synth_field_sections(0x5EED0E0 + nsec, nsec)
+    dst, secs = enc.encode_sections(plain, strs, lines, line_start)
+    assert dst.tobytes() == src.tobytes()
+    assert (secs["off"] == blocks["off"]).all() and (secs["len"] == blocks["len"]).all()
+
+
 def test_encode_sections_device_resident(enc):
     import torch
     src, blocks, plain, strs, lines, line_start = qpack.synth_field_sections(0x5EED0C5, 2000)
