@@ -9,8 +9,9 @@ namespace qhk {
 // out of the product library.
 #ifdef QH_STAMPS
 __device__ unsigned long long g_stamps[16];
-// per block (blockIdx.x < 8192): start (realtime), lifetime, HW_ID register
-__device__ unsigned long long g_blk[8192][3];
+// per block (blockIdx.x < 8192): start (realtime), lifetime (realtime,
+// 100 MHz), HW_ID register, lifetime in shader clocks (s_memtime)
+__device__ unsigned long long g_blk[8192][4];
 #define QH_ST_INIT()                                                         \
   unsigned long long _st_t = __builtin_amdgcn_s_memtime(), _st_a[16] = {0};
 #define QH_ST(k)                                                             \
@@ -59,6 +60,7 @@ struct StampAcc {
         g_blk[blockIdx.x][0] = r0;
         g_blk[blockIdx.x][1] = life;
         g_blk[blockIdx.x][2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_blk[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - t0;
       }
     }
     if (threadIdx.x == 0)

@@ -34,10 +34,10 @@ def main():
     for _ in range(3):
         run()
     codec.sync()
-    buf = (ctypes.c_uint64 * (8192 * 3))()
+    buf = (ctypes.c_uint64 * (8192 * 4))()
     lib.qh_debug_blocks.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     assert lib.qh_debug_blocks(buf, 8192) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 3).astype(np.int64)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 4).astype(np.int64)
     a = a[a[:, 1] > 0]
     t0 = a[:, 0].min()
     st = (a[:, 0] - t0) / 100.0
@@ -51,6 +51,10 @@ def main():
           f"p50 {np.median(life):.1f} p90 {np.percentile(life, 90):.1f} max {life.max():.1f} us  "
           f"end max {(st + life).max():.1f} us")
     bx = np.arange(len(a))
+    # shader clock per block: s_memtime ticks / realtime (100 MHz) ticks
+    mhz = a[:, 3] / np.maximum(a[:, 1], 1) * 100.0
+    print("  clock MHz by blockIdx%8: " + "  ".join(
+        f"{k}:{np.mean(mhz[bx % 8 == k]):.0f}" for k in range(8)))
     for name, key in (("blockIdx%8", bx % 8), ("se", se), ("sh", sh)):
         g = defaultdict(list)
         for k, v in zip(key, life):
