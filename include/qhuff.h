@@ -174,6 +174,11 @@ QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
  * fastest for skewed or long strings (Zipf up to 4 KiB: 2.3x). */
 #define QH_ENCODER_WINDOWS 0
 #define QH_ENCODER_WAVES 1
+/* QH_ENCODER_FUSED: one pass over the plaintext -- every lane takes 16 bytes
+ * of one string, whatever the string lengths; code bits are summed per
+ * string, a decoupled look-back over 4 KiB tiles places each tile in the dense
+ * output, and the codes go out through an LDS stage. */
+#define QH_ENCODER_FUSED 2
 QH_EXPORT int qh_ctx_set_encoder(qh_ctx *ctx, int kind);
 QH_EXPORT void *qh_ctx_stream(qh_ctx *ctx);
 /* Wait for all work queued on the context's stream. */

@@ -59,6 +59,7 @@
 #endif
 #include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes: the default)
 #include "qh_enc_waves.inc"   // encoder codes (QH_ENCODER_WAVES): per-wave chunks, LDS rings
+#include "qh_enc_fused.inc"   // encoder, lengths + codes in one pass (QH_ENCODER_FUSED)
 #ifdef QH_DEV_VARIANTS
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
 #endif

@@ -176,7 +176,8 @@ class HuffmanBatchCodec:
     def set_encoder(self, kind: str):
         """'windows' (default: strings of similar length) or 'waves' (skewed
         or long strings); results are identical."""
-        k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES}[kind]
+        k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES,
+             "fused": _lib.QH_ENCODER_FUSED}[kind]
         _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")
 
     def sync(self):

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Time the shipped encoders (windows, waves) on a BASELINE-shaped batch and
+"""Time the shipped encoders (windows, waves, fused) on a BASELINE-shaped batch and
 check their bytes agree (development tool, one GPU).
 Usage: python scripts/enc_variants.py [--n N] [--alphabet A|U] [--zipf]"""
 import argparse
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--alphabet", default="A")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--zipf", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated encoders (default: all)")
     args = ap.parse_args()
     import torch
     from nghttp3_amd import HuffmanBatchCodec, synth
@@ -31,7 +32,8 @@ def main():
     ln = spans[:, 1] & 0xFFFFFFFF
     bound = int(((ln * 30 + 7) // 8).sum().item())
     ref = None
-    for kind in ("windows", "waves"):
+    kinds = [k for k in ("windows", "waves", "fused") if not args.only or k in args.only.split(",")]
+    for kind in kinds:
         c.set_encoder(kind)
         enc = torch.zeros(bound, dtype=torch.uint8, device="cuda")
         eout = torch.empty((n, 2), dtype=torch.int64, device="cuda")

@@ -354,12 +354,13 @@ def test_synth_device_matches_host(codec):
 
 @pytest.mark.parametrize("name,decoder", [("c2_A", "windows"), ("c2_U", "windows"),
                                           ("c3_A", "windows"), ("c3_A", "waves"),
-                                          ("c2_U", "waves")])
+                                          ("c2_U", "waves"), ("c3_A", "fused"),
+                                          ("c2_U", "fused")])
 def test_full_size_config(codec, digests, name, decoder):
     """BASELINE configs at full size (2^20 strings): synth digest, encode
     digest vs the oracle's, then decode round trip (size-independent), with
-    either shipped decoder."""
-    codec.set_decoder(decoder)
+    either shipped decoder ("fused": the fused encoder, window decoder)."""
+    codec.set_decoder(decoder if decoder != "fused" else "windows")
     codec.set_encoder(decoder)
     try:
         _full_size_config(codec, digests, name)
@@ -656,7 +657,7 @@ def test_decoder_variants(kind, corpus, errors, kat, codec):
 
 
 def _long_mode_batch(rng):
-    """Strings that drive the window decoder's long iterations (V & 256):
+    """Strings that drive the window decoder's long iterations (pkv::kLongCodes, qh_dec_common.inc):
     binary text, binary then header text and back, errors met inside long
     iterations (an EOS code mid-string, a cut last code, bad padding), and
     header text sharing windows with them."""
@@ -790,7 +791,7 @@ def test_zipf_lengths_roundtrip(codec, alphabet):
 # sorted 256-string window per workgroup, LDS stage, coalesced copy-out) and
 # the wave encoder (per-wave sorted chunks, LDS rings, per-lane 16-byte
 # output chunks).
-ENCODERS = ["windows", "waves"]
+ENCODERS = ["windows", "waves", "fused"]
 
 
 @pytest.mark.parametrize("kind", ENCODERS)

@@ -120,3 +120,16 @@ def test_driver_gpu_config1_round_trip(tmp_path):
     assert r.returncode == 0, r.stderr
     assert back == t
     assert '"path": "gpu"' in r.stderr
+
+
+def test_driver_gpu_netbsd_summary_matches_reference_cli(tmp_path):
+    """The GPU path prints the reference CLI's summary line for the corpus QIF
+    at -s 0 (examples/qpack_encode.cc:209-216) and writes the
+    scalar path's bytes."""
+    from test_qif import REFERENCE_NETBSD_S0_LINE
+    data = open(os.path.join(GOLDEN, "netbsd.qif"), "rb").read()
+    r, out = _run(tmp_path, ["-s", "0", "encode"], data)
+    assert r.returncode == 0, r.stderr
+    assert REFERENCE_NETBSD_S0_LINE in r.stderr.strip().splitlines()
+    r2, out2 = _run(tmp_path, ["--scalar", "-s", "0", "encode"], data, "scalar")
+    assert r2.returncode == 0 and out == out2

@@ -182,3 +182,18 @@ def test_driver_scalar_failures(tmp_path, case):
 def test_driver_rejects_dynamic_table_encoding(tmp_path):
     r, _ = _run(tmp_path, ["--scalar", "-s", "256", "encode"], b"a\tb\n\n")
     assert r.returncode != 0 and "-s 0" in r.stderr
+
+
+# The reference CLI's own summary line for this corpus at -s 0 (BASELINE.md,
+# "CLI-reported compression": examples/qpack_encode.cc:209-216 printed it in
+# the survey's run of the compiled reference): encoded bytes of the
+# netbsd QIF's 18 sections, all on the request stream, nothing on the
+# encoder stream.
+REFERENCE_NETBSD_S0_LINE = "5376 -> 2934 (r:2934 + e:0) 45.42% compressed"
+
+
+def test_driver_scalar_netbsd_summary_matches_reference_cli(tmp_path):
+    r, out = _run(tmp_path, ["--scalar", "-s", "0", "encode"], open(NETBSD_QIF, "rb").read())
+    assert r.returncode == 0, r.stderr
+    assert r.stderr.strip().splitlines()[-1] == REFERENCE_NETBSD_S0_LINE
+    assert len(out) == 2934 + 12 * 18  # request records: 12-byte header each
