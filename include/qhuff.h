@@ -164,6 +164,11 @@ QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
  * 4 KiB: 2.2x the window decoder). */
 #define QH_DECODER_WINDOWS 0
 #define QH_DECODER_WAVES 1
+/* QH_DECODER_SORTED: the window decoder over a batch-wide schedule -- two
+ * passes over the spans sort the strings into 16-byte length classes,
+ * longest first, so every 256-string window holds strings of one class
+ * (fastest for skewed lengths; same output layout). */
+#define QH_DECODER_SORTED 2
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 /* Codes kernel of qh_encode_batch (results are identical; speed is not):
  * QH_ENCODER_WINDOWS (default) encodes a sorted window of up to 256 strings

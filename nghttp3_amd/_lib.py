@@ -25,6 +25,7 @@ QH_WHERE_HOST = 0
 QH_WHERE_DEVICE = 1
 QH_DECODER_WINDOWS = 0
 QH_DECODER_WAVES = 1
+QH_DECODER_SORTED = 2
 QH_ENCODER_WINDOWS = 0
 QH_ENCODER_WAVES = 1
 QH_ENCODER_FUSED = 2

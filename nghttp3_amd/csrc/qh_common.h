@@ -64,8 +64,8 @@ struct StampAcc {
       }
     }
     if (threadIdx.x == 0)
-      for (int k = 0; k < 14; ++k)
-        if (a[k]) atomicAdd(&g_stamps[k], a[k]);
+      for (int k = 0; k < 16; ++k)
+        if (a[k] && k != 14) atomicAdd(&g_stamps[k], a[k]);
   }
 };
 #else
@@ -138,6 +138,16 @@ __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
 }
 __device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations are
+// complete (lgkmcnt(0)), its global loads and stores may stay in flight.
+// (__syncthreads() also waits for every outstanding global store -- a round
+// trip to memory per barrier in a kernel that streams its output.)  The
+// asm's memory clobber keeps the compiler from moving memory accesses
+// across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <typename T>

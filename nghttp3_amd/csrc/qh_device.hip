@@ -45,6 +45,7 @@
 #include "qh_scan.inc"       // batch prefix sum (synthetic inputs)
 #include "qh_dec_common.inc"  // decode table blob, slot reservation
 #include "qh_check.inc"       // field name / value checks (device)
+#include "qh_sched.inc"       // batch-wide length-class schedule (QH_DECODER_SORTED)
 #ifdef QH_DEV_VARIANTS         // development variants (make dev): not shipped
 #include "qh_lane_dec.inc"   // decoder: 4-bit FSM, one string per lane
 #include "qh_lane_dec2.inc"  // decoder: 4-bit FSM, two strings per lane

@@ -170,7 +170,8 @@ class HuffmanBatchCodec:
     def set_decoder(self, kind: str):
         """'windows' (default: strings of similar length) or 'waves' (skewed
         lengths, e.g. Zipf up to 4 KiB); results are identical."""
-        k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES}[kind]
+        k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES,
+             "sorted": _lib.QH_DECODER_SORTED}[kind]
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
 
     def set_encoder(self, kind: str):

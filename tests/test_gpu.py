@@ -355,13 +355,15 @@ def test_synth_device_matches_host(codec):
 @pytest.mark.parametrize("name,decoder", [("c2_A", "windows"), ("c2_U", "windows"),
                                           ("c3_A", "windows"), ("c3_A", "waves"),
                                           ("c2_U", "waves"), ("c3_A", "fused"),
-                                          ("c2_U", "fused")])
+                                          ("c2_U", "fused"), ("c3_A", "sorted"),
+                                          ("c2_U", "sorted")])
 def test_full_size_config(codec, digests, name, decoder):
     """BASELINE configs at full size (2^20 strings): synth digest, encode
     digest vs the oracle's, then decode round trip (size-independent), with
-    either shipped decoder ("fused": the fused encoder, window decoder)."""
+    either shipped decoder ("fused": the fused encoder, window decoder;
+    "sorted": the window encoder, the sorted decoder)."""
     codec.set_decoder(decoder if decoder != "fused" else "windows")
-    codec.set_encoder(decoder)
+    codec.set_encoder(decoder if decoder != "sorted" else "windows")
     try:
         _full_size_config(codec, digests, name)
     finally:
@@ -406,14 +408,15 @@ def _full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
-@pytest.mark.parametrize("decoder", ["windows", "waves"])
+@pytest.mark.parametrize("decoder", ["windows", "waves", "sorted"])
 def test_config5_rank_shard_full_size(codec, digests, decoder):
     """Config 5 at size: rank 0's shard of 16M Zipf strings split by bytes
     over 8 GPUs (2.1M strings, 438 MB, lengths 1..4096), as bench.py cuts
     it: the device generator from the global byte offset, encode digests vs
     the oracle's, then the decode round trip (chunked compare)."""
     codec.set_decoder(decoder)
-    codec.set_encoder(decoder)  # the shipped kernel pair for skewed lengths
+    # the shipped kernel pairs for skewed lengths
+    codec.set_encoder({"windows": "windows", "waves": "waves", "sorted": "fused"}[decoder])
     try:
         _config5_rank_shard(codec, digests)
     finally:
@@ -573,7 +576,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
 
 # The two shipped decoders (qh_ctx_set_decoder); the development variants
 # (make dev) are timed by scripts/dec_variants.py, not shipped.
-DECODERS = ["windows", "waves"]
+DECODERS = ["windows", "waves", "sorted"]
 # (development: QHUFF_LIB=nghttp3_amd/lib/libqhuff_dev.so QH_TEST_DEV_DECODERS=
 # peek11su,... adds those variants of the development build to these tests)
 DECODERS += ["dev:" + k for k in os.environ.get("QH_TEST_DEV_DECODERS", "").split(",") if k]
