@@ -83,3 +83,11 @@ clean:
 	rm -f $(LIBDIR)/*.o $(DRIVER) $(LIB) $(ARCHIVE) $(STAMPS) $(DEV) $(ORACLE)
 
 .PHONY: all clean stamps
+
+# Fused-encoder ablation builds (timing experiments; wrong bytes):
+# make abl ABL=<mask> -> libqhuff_abl<mask>.so (qh_enc_fused.inc QH_EW_ABL)
+ABL ?= 0
+abl: $(LIBDIR)/libqhuff_abl$(ABL).so
+$(LIBDIR)/libqhuff_abl$(ABL).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_EW_ABL=$(ABL) -c $< -o $(LIBDIR)/qh_device_abl$(ABL).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_abl$(ABL).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

@@ -55,6 +55,7 @@ int main() {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const int steps = 4096;
+  double best = 0, w4c1 = 0;  // lookups/s: best of all shapes; 4 waves/SIMD, one chain per lane
   for (int store = 0; store < 2; ++store)
     for (int bpc : {2, 4, 8}) {
       const size_t lds = 160 * 1024 / bpc - 1024;  // limits blocks per CU
@@ -73,7 +74,12 @@ int main() {
         printf("store %d waves/SIMD %d chains %d: %6.1f cyc/step/wave  %.2f lookups/cyc/CU\n",
                store, bpc, chains, cyc / steps,
                (double)grid * 256 * steps * chains / (cyc * ncu));
+        const double rate = (double)grid * 256 * steps * chains / (ms * 1e-3);
+        if (rate > best) best = rate;
+        if (!store && bpc == 4 && chains == 1) w4c1 = rate;
       }
     }
+  printf("{\"chained_lookups_per_s_best\": %.4e, \"chained_lookups_per_s_4waves_1chain\": %.4e, \"cus\": %d}\n",
+         best, w4c1, ncu);
   return 0;
 }
