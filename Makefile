@@ -59,19 +59,19 @@ $(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(L
 # points at it).
 STAMPS := $(LIBDIR)/libqhuff_stamps.so
 stamps: $(STAMPS)
-$(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
-	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -DQH_DEV_VARIANTS -c $< -o $(LIBDIR)/qh_device_stamps.o
+$(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc dev/csrc/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -DQH_STEP_COUNTS=1 -DQH_DEV_VARIANTS -Idev/csrc -c $< -o $(LIBDIR)/qh_device_stamps.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_stamps.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
 # Development build with every kernel variant (-DQH_DEV_VARIANTS: decoders
 # fsm / fsm2 / lut / run / other peek widths and queue shapes, the
 # chunk-engine and streaming encoders), selected by QHUFF_DECODER /
 # QHUFF_ENCODER / QHUFF_CODES; loaded only when QHUFF_LIB points at it
-# (scripts/dec_variants.py).
+# (dev/scripts/dec_variants.py).
 DEV := $(LIBDIR)/libqhuff_dev.so
 dev: $(DEV)
-$(DEV): $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
-	$(HIPCC) $(HIPFLAGS) -DQH_DEV_VARIANTS -c $< -o $(LIBDIR)/qh_device_dev.o
+$(DEV): $(CSRC)/qh_device.hip $(CSRC)/*.inc dev/csrc/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_DEV_VARIANTS -Idev/csrc -c $< -o $(LIBDIR)/qh_device_dev.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_dev.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
 # Oracle: -O2 -mavx2 as nghttp3's README.rst:61-67 prescribes for the

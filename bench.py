@@ -130,6 +130,38 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+STEPS_JSON = os.path.join(ROOT, "profiles", "r03", "decoder_steps.json")
+CHAIN_JSON = os.path.join(ROOT, "profiles", "r03", "lds_chain.json")
+LDS_B32_TBPS = 75.0  # ds_read_b32 aggregate, every CU streaming (MI355X_MICROARCH.md LDS section)
+
+
+def lds_secondary(kernel, avg_us, n, args):
+    """The decoder's second ceiling: its table lookups per launch (16 per
+    lock-step iteration of a lane, counted by the instrumented build on this
+    workload: dev/scripts/decoder_steps.py) over its time, against the measured
+    rate of dependent LDS lookup chains (dev/ubench/lds_chain.hip, best
+    occupancy) and the guide's ds_read_b32 aggregate."""
+    if kernel != "qh_k_dec_peek" or args.alphabet != "A" or args.min_len != 8 or args.max_len != 256:
+        return None
+    try:
+        st = json.load(open(STEPS_JSON))["workloads"]["config3_A"]
+        chain = json.load(open(CHAIN_JSON))
+    except Exception:
+        return None
+    if st["strings"] != n:
+        return None
+    lookups = st["sorted"]["lookups"]
+    rate = lookups / (avg_us * 1e-6)
+    agg = LDS_B32_TBPS * 1e12 / 4
+    return {"unit": "lookups/s", "lookups_per_launch": lookups, "achieved": round(rate, -6),
+            "chained_rate": chain["chained_lookups_per_s_best"],
+            "frac_of_chained_rate": round(rate / chain["chained_lookups_per_s_best"], 4),
+            "ds_read_b32_aggregate": agg, "frac_of_aggregate": round(rate / agg, 4),
+            "active_lane_frac": st["sorted"]["active_lane_frac"],
+            "source": "profiles/r03/decoder_steps.json (make stamps, QH_STEP_COUNTS), "
+                      "profiles/r03/lds_chain.json"}
+
+
 def _cpu_model():
     try:
         for ln in open("/proc/cpuinfo"):
@@ -255,6 +287,9 @@ def main():
             "qh_k_enc_lens_stream": plain + 16 * n + 8 * n,  # D + spans in + len/status out
             "qh_k_enc_lens_lane": plain + 16 * n + 8 * n,
             "qh_k_enc_lanes": plain + encb + 16 * n + 8 * n + 16 * n,  # D + E + spans
+            "qh_k_encw": plain + encb + 16 * n + 16 * n,     # D + E + spans in + out
+            "qh_k_sched_count": 16 * n,                      # spans in
+            "qh_k_sched_scatter": 16 * n + 24 * n,           # spans in, records out
         }
         kern = {}
         for name, (cnt, ms) in ktimes.items():
@@ -283,6 +318,11 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "algo_bytes_per_launch": kern[dom]["algo_bytes"],
                     "avg_us": kern[dom]["avg_us"]}
+        sec = lds_secondary(dom, kern[dom]["avg_us"], n, args)
+        if sec:
+            roofline["secondary"] = sec
+            if sec["frac_of_chained_rate"] > roofline["frac"]:
+                roofline["bound"] = "lds-chain"
 
     # ---- config 5: 16M Zipf strings (s = 1.2, 1..4096 B), split by bytes ----
     config5 = None
@@ -293,23 +333,24 @@ def main():
         sp5, tot5 = codec.spans_to_device(ln5[c0:c1])
         src5 = codec.synth_fill(SEED5, f5, tot5, synth.ALPHABET_A)
         enc5, eout5, eb5, dec5, dout5 = buffers(src5, sp5)
-        # skewed lengths: the wave decoder (QH_DECODER_WAVES); the window
-        # decoder's time on the same batch is reported beside it
-        td5_win = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 3)
-        ok5_win = roundtrip_ok(src5, sp5, dec5, dout5)
+        # the shipped decoder (QH_DECODER_SORTED: the length-class schedule)
+        # and the one-pass encoder (QH_ENCODER_FUSED); the wave decoder's and
+        # the window encoder's times on the same batch are reported beside
+        # them, and their bytes must agree
         codec.set_decoder("waves")
+        td5_alt = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 3)
+        ok5_alt = roundtrip_ok(src5, sp5, dec5, dout5)
+        codec.set_decoder("sorted")
         dec5.zero_()
         codec.decode_dev(enc5, eout5, dec5, dout5)
-        ok5 = roundtrip_ok(src5, sp5, dec5, dout5) and ok5_win
-        # and the wave encoder (QH_ENCODER_WAVES): its bytes must be the
-        # window encoder's; the window encoder's time is reported beside it
-        te5_win = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 3)
-        enc5_win, eout5_win = enc5[:eb5].clone(), eout5.clone()
-        codec.set_encoder("waves")
+        ok5 = roundtrip_ok(src5, sp5, dec5, dout5) and ok5_alt
+        te5_alt = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 3)
+        enc5_alt, eout5_alt = enc5[:eb5].clone(), eout5.clone()
+        codec.set_encoder("fused")
         enc5.zero_()
         codec.encode_dev(src5, sp5, enc5, eout5)
-        ok5 = ok5 and bool(torch.equal(enc5[:eb5], enc5_win)) and bool(torch.equal(eout5, eout5_win))
-        del enc5_win, eout5_win
+        ok5 = ok5 and bool(torch.equal(enc5[:eb5], enc5_alt)) and bool(torch.equal(eout5, eout5_alt))
+        del enc5_alt, eout5_alt
         te5 = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 5)
         td5 = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 5)
         codec.enable_timing(True)
@@ -317,7 +358,6 @@ def main():
             codec.decode_dev(enc5, eout5, dec5, dout5)
         k5 = kernel_table(codec.kernel_times(), sp5.shape[0], tot5, eb5)
         codec.enable_timing(False)
-        codec.set_decoder("windows")
         codec.set_encoder("windows")
         d5 = k5.get("qh_k_dec_peek", {})
         p5, e5 = D.sum(float(tot5)), D.sum(float(eb5))
@@ -327,10 +367,11 @@ def main():
                               "mean %.1f B" % float(ln5.mean()),
                    "shards": world, "strings_rank0": int(c1 - c0) if rank == 0 else None,
                    "encode_GiBps": round(p5 / te5 / GIB, 2), "decode_GiBps": round(p5 / td5 / GIB, 2),
-                   "decoder": "waves (qh_k_dec_peekw: per-wave sorted chunks, LDS-ring input)",
-                   "decode_GiBps_window_decoder": round(p5 / D.max(td5_win) / GIB, 2),
-                   "encoder": "waves (qh_k_enc_waves: per-wave sorted chunks, LDS-ring output)",
-                   "encode_GiBps_window_encoder": round(p5 / D.max(te5_win) / GIB, 2),
+                   "decoder": "sorted (default: length-class schedule + qh_k_dec_peek windows)",
+                   "decode_GiBps_wave_decoder": round(p5 / D.max(td5_alt) / GIB, 2),
+                   "encoder": "fused (qh_k_encw: lengths and codes in one pass over the plaintext)",
+                   "encode_GiBps_window_encoder": round(p5 / D.max(te5_alt) / GIB, 2),
+                   "decode_kernels_us_rank0": {k: v["avg_us"] for k, v in k5.items()},
                    "round_trip_GiBps": round(p5 / (te5 + td5) / GIB, 2),
                    "decode_kernel_us_rank0": d5.get("avg_us"),
                    "decode_kernel_GBps_min_rank": round(-dec_gbps_min, 1),
@@ -353,20 +394,26 @@ def main():
     if rank == 0 and world == 1 and not args.no_configs:
         u_src, u_spans, u_total = codec.synth(args.seed, args.strings, args.min_len, args.max_len, synth.ALPHABET_U)
         u_enc, u_eout, u_eb, u_dec, u_dout = buffers(u_src, u_spans)
+        tue_win = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 3)
+        codec.set_encoder("fused")  # (binary text: the one-pass encoder)
+        u_enc.zero_()
+        codec.encode_dev(u_src, u_spans, u_enc, u_eout)
         codec.decode_dev(u_enc, u_eout, u_dec, u_dout)
         u_ok = roundtrip_ok(u_src, u_spans, u_dec, u_dout)
         tue = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 5)
         tud = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 5)
+        codec.set_encoder("windows")
         configU = {"strings": args.strings, "plain_bytes": u_total, "enc_bytes": u_eb,
-                   "encode_GiBps": round(u_total / tue / GIB, 2),
-                   "decode_GiBps": round(u_total / tud / GIB, 2),
+                   "encode_GiBps": round(u_total / tue / GIB, 2), "encoder": "fused",
+                   "encode_GiBps_window_encoder": round(u_total / tue_win / GIB, 2),
+                   "decode_GiBps": round(u_total / tud / GIB, 2), "decoder": "sorted (default)",
                    "round_trip_GiBps": round(u_total / (tue + tud) / GIB, 2), "bit_exact": u_ok}
         del u_src, u_spans, u_enc, u_eout, u_dec, u_dout
 
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None
     if rank == 0 and world == 1 and not args.no_host_path:
-        host_path = leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n)
+        host_path = leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev)
 
     # ---- CPU baseline (rank 0, N = 1) ----
     cpu = None
@@ -547,12 +594,85 @@ def leg_config1():
     return res
 
 
-def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n):
+def _gpu_numa(torch, dev):
+    """The GPU's NUMA node and that node's CPUs (sysfs), or (None, None)."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read().strip())
+        if node < 0:
+            return None, None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        return node, cpus
+    except Exception:
+        return None, None
+
+
+def _page_node(t):
+    """NUMA node of the page holding a host tensor's first byte (move_pages),
+    or None."""
+    try:
+        import ctypes
+        libc = ctypes.CDLL(None, use_errno=True)
+        pages = (ctypes.c_void_p * 1)(t.data_ptr())
+        status = (ctypes.c_int * 1)(-1)
+        rc = libc.syscall(279, 0, 1, pages, None, status, 0)  # SYS_move_pages (x86_64), query only
+        return int(status[0]) if rc == 0 and status[0] >= 0 else None
+    except Exception:
+        return None
+
+
+def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
     """Decode from host memory: H2D of spans and encoded bytes, kernels, D2H
-    of results (pageable and pinned buffers)."""
+    of results (pageable and pinned buffers), beside a copy-engine probe of
+    the same byte counts in the same run (H2D alone, D2H alone, both at once
+    on two streams).  The host buffers are allocated with this process bound
+    to the GPU's NUMA node's CPUs (first touch places them there); the node of
+    each pinned buffer's pages is recorded."""
+    node, cpus = _gpu_numa(torch, dev)
+    try:
+        aff0 = os.sched_getaffinity(0)
+    except Exception:
+        aff0 = None
+    if cpus and aff0 and cpus & aff0:
+        os.sched_setaffinity(0, cpus & aff0)
     eo = eout.cpu().numpy()
     cap_h = int(q.decode_slot_size(eo[:, 1] & 0xFFFFFFFF).sum())
-    out = {}
+    in_bytes, out_bytes = enc_bytes + 16 * n, total + 16 * n
+    out = {"gpu_numa_node": node, "bound_cpus": len(cpus & aff0) if cpus and aff0 else None,
+           "bytes_in": in_bytes, "bytes_out": out_bytes}
+    # copy-engine probe: the path's byte counts, pinned, 3 reps each
+    h_in = torch.empty(in_bytes, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(out_bytes, dtype=torch.uint8, pin_memory=True)
+    h_in.fill_(1)
+    h_out.fill_(1)
+    d_in = torch.empty(in_bytes, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(out_bytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def probe(h2d, d2h, reps=3):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    d_in.copy_(h_in, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    h_out.copy_(d_out, non_blocking=True)
+            torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps
+
+    probe(True, True, 1)
+    t_h2d, t_d2h, t_both = probe(True, False), probe(False, True), probe(True, True)
+    out["probe"] = {"h2d_GBps": round(in_bytes / t_h2d / 1e9, 2), "d2h_GBps": round(out_bytes / t_d2h / 1e9, 2),
+                    "both_ms": round(t_both * 1e3, 3),
+                    "both_GBps_each": [round(in_bytes / t_both / 1e9, 2), round(out_bytes / t_both / 1e9, 2)],
+                    "pinned_page_node": [_page_node(h_in), _page_node(h_out)]}
+    del h_in, h_out, d_in, d_out
     for kind in ("pageable", "pinned"):
         pin = kind == "pinned"
         e_t = torch.empty(enc_bytes, dtype=torch.uint8, pin_memory=pin)
@@ -571,7 +691,13 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n):
         t_host = (time.perf_counter() - a) / reps
         out[kind] = {"decode_GiBps_incl_h2d_d2h": round(total / t_host / GIB, 2),
                      "ms": round(t_host * 1e3, 2)}
+        if pin:
+            out[kind]["page_node"] = [_page_node(e_t), _page_node(d_t)]
+            # the bound: both directions at once, the probe's time for these bytes
+            out[kind]["frac_of_probe_both"] = round(t_both / t_host, 3)
         del e_t, sp_t, d_t, o_t
+    if aff0:
+        os.sched_setaffinity(0, aff0)
     return out
 
 

@@ -47,6 +47,7 @@ def main():
         dec.zero_()
         c.decode_dev(enc, eout, dec, dout)
         st = c.stats()
+        alf = round(st["lane_steps"] / (64 * st["wave_steps"]), 4) if st.get("wave_steps") else None
         ok = st["n_errors"] == 0 and st["out_bytes"] == total and \
             bool(((dout[:, 1] & 0xFFFFFFFF) == ln).all())
         # spot-check the bytes of a strided subset
@@ -56,6 +57,14 @@ def main():
             torch.repeat_interleave(torch.cumsum(l, 0) - l, l)
         ok = ok and bool((dec[torch.repeat_interleave(dout[idx, 0], l) + pos] ==
                           src[torch.repeat_interleave(spans[idx, 0], l) + pos]).all())
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            c.decode_dev(enc, eout, dec, dout)
+        e1.record()
+        torch.cuda.synchronize()
+        wall_us = e0.elapsed_time(e1) * 1e3 / args.reps
         c.enable_timing(True)
         for _ in range(args.reps):
             c.decode_dev(enc, eout, dec, dout)
@@ -64,10 +73,11 @@ def main():
         ks = {k: round(ms / max(cnt, 1) * 1e3, 2) for k, (cnt, ms) in kt.items()}
         dk = ks.get("qh_k_dec_peek", 0.0)
         print(json.dumps({"decoder": kind, "alphabet": args.alphabet, "zipf": args.zipf, "n": n,
-                          "kernels_us": ks, "sum_us": round(sum(ks.values()), 2),
+                          "kernels_us": ks, "sum_us": round(sum(ks.values()), 2), "wall_us": round(wall_us, 2),
+                          "wall_GiBps": round(total / (wall_us * 1e-6) / 2**30, 1),
                           "plain_GiBps": round(total / (sum(ks.values()) * 1e-6) / 2**30, 1),
                           "decoder_frac": round((ebytes + total + 32 * n) / (dk * 1e-6) / 8e12, 4) if dk else None,
-                          "ok": ok}), flush=True)
+                          "active_lane_frac": alf, "lane_steps": st.get("lane_steps"), "ok": ok}), flush=True)
 
 
 if __name__ == "__main__":

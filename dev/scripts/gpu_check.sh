@@ -1,12 +1,12 @@
 #!/bin/bash
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats.
 # Every GPU step has its own time limit; a crash/fault/timeout ends the
-# script (no further GPU work).  Usage: scripts/gpu_check.sh TAG [STEPS...]
+# script (no further GPU work).  Usage: dev/scripts/gpu_check.sh TAG [STEPS...]
 # steps: test smoke bench prof pmc (default: test smoke bench prof)
 set -u
 TAG=${1:-r01}; shift || true
 STEPS=${*:-test smoke bench prof}
-ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"

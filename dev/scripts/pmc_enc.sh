@@ -1,8 +1,8 @@
 #!/bin/bash
 # SQ + memory-path PMC groups over bench.py --profile-only (one rocprofv3
-# --pmc pass per group, each under its own limit).  Usage: scripts/pmc_enc.sh TAG
+# --pmc pass per group, each under its own limit).  Usage: dev/scripts/pmc_enc.sh TAG
 set -u
-ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=${1:-pmcenc}
 OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
@@ -18,5 +18,5 @@ for group in \
   rc=$?; echo "group $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/g$i.log"; exit $rc; fi
 done
-python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E 'qhk' | sed 's/  /\n   /g' > "$OUT/summary.txt"
+python3 "$ROOT/dev/scripts/pmc_summary.py" "$OUT" | grep -E 'qhk' | sed 's/  /\n   /g' > "$OUT/summary.txt"
 cat "$OUT/summary.txt"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Memory-path counters (L1/TLB/L2) for bench.py --profile-only.
 set -u
-ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=$1
 OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
@@ -17,4 +17,4 @@ for group in \
   rc=$?; echo "group $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/g$i.log"; exit $rc; fi
 done
-python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E 'qhk' | sed 's/  /\n   /g'
+python3 "$ROOT/dev/scripts/pmc_summary.py" "$OUT" | grep -E 'qhk' | sed 's/  /\n   /g'

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Collect SQ counter groups (one rocprofv3 --pmc pass each) for bench.py --profile-only.
 set -u
-ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=${1:-pmc}; shift
 OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counter groups for one decoder configuration (env passed through).
 set -u
-ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=$1; KIND=$2
 OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
@@ -12,8 +12,8 @@ for group in \
   "SQ_LDS_ADDR_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_LDS_UNALIGNED_STALL SQ_IFETCH_LEVEL SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_BUSY_CU_CYCLES" ; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $group --output-format csv -d "$OUT/g$i" -o run -- \
-     python3 "$ROOT/scripts/dec_variants.py" --kinds "$KIND" --reps 2 > "$OUT/g$i.log" 2>&1
+     python3 "$ROOT/dev/scripts/dec_variants.py" --kinds "$KIND" --reps 2 > "$OUT/g$i.log" 2>&1
   rc=$?; echo "group $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/g$i.log"; exit $rc; fi
 done
-python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E 'dec_run|dec_peek' | tr ' ' '\n'
+python3 "$ROOT/dev/scripts/pmc_summary.py" "$OUT" | grep -E 'dec_run|dec_peek' | tr ' ' '\n'

@@ -145,6 +145,13 @@ typedef struct qh_batch_stats {
   uint64_t out_bytes;  /* sum of output lengths (successful strings) */
   uint64_t dst_bytes;  /* destination bytes the layout occupies      */
   uint64_t n_errors;   /* strings with status != 0                   */
+  /* decode with QH_DECODER_WINDOWS / _SORTED: lock-step iterations (16
+   * table lookups each) run by lanes, and by waves (each wave counts its
+   * longest lane per window); lane_steps / (64 * wave_steps) is the active-
+   * lane fraction.  Counted only by the instrumented development build
+   * (make stamps: the counter slows the decoder); 0 otherwise. */
+  uint64_t lane_steps;
+  uint64_t wave_steps;
 } qh_batch_stats;
 
 typedef struct qh_ctx qh_ctx;
@@ -156,18 +163,17 @@ QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream);
 QH_EXPORT void qh_ctx_del(qh_ctx *ctx);
 QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
 /* Decoder kernel of qh_decode_batch (results are identical; speed is not):
- * QH_DECODER_WINDOWS (default) sorts 256-string windows by length and
- * decodes a window per workgroup -- fastest for strings of similar length
- * (headers of 8-256 B); QH_DECODER_WAVES lets every wave sort and decode
- * its own chunks of 256 strings with no workgroup barrier, its input staged
- * through LDS in 64-byte groups -- fastest for skewed lengths (Zipf up to
- * 4 KiB: 2.2x the window decoder). */
+ * QH_DECODER_WINDOWS sorts each 256-string window by length and decodes a
+ * window per workgroup; QH_DECODER_WAVES lets every wave sort and decode its
+ * own chunks of 256 strings with no workgroup barrier, its input staged
+ * through LDS in 64-byte groups. */
 #define QH_DECODER_WINDOWS 0
 #define QH_DECODER_WAVES 1
-/* QH_DECODER_SORTED: the window decoder over a batch-wide schedule -- two
- * passes over the spans sort the strings into 16-byte length classes,
- * longest first, so every 256-string window holds strings of one class
- * (fastest for skewed lengths; same output layout). */
+/* QH_DECODER_SORTED (default): the window decoder over a batch-wide
+ * schedule -- passes over the spans sort the strings into 16-byte length
+ * classes, longest first, so every 256-string window holds strings of one
+ * class (same output layout).  On one MI355X: 8-256 B headers as fast as
+ * QH_DECODER_WINDOWS, binary text 1.3x, Zipf lengths to 4 KiB 4.6x. */
 #define QH_DECODER_SORTED 2
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 /* Codes kernel of qh_encode_batch (results are identical; speed is not):
@@ -373,7 +379,14 @@ QH_EXPORT int qh_scan_blocks_batch(qh_ctx *ctx, const uint8_t *src,
  *   dst        -- decoded Huffman strings, qh_decode_batch's slot layout in
  *                 Huffman-string order; dst_cap >= the `dst_need` total.
  * status[b] is 0 or the reference's error for the block: its first framing
- * error, unless a Huffman string before it fails (-401).
+ * error, unless a Huffman string before it fails (-401).  A block whose
+ * framing failed has no lines (its line_start range is empty) and keeps the
+ * spans read before the error; a block that framed cleanly but whose
+ * Huffman string failed (-401) keeps all its lines and spans -- the framing
+ * is valid, the string's strs[k].status says which one failed -- where the
+ * reference emits no field of it (the callers drop such a block's lines).
+ * On QH_ERR_NOMEM the framing may have written lines and spans below the
+ * caps; nothing else is written.
  * Totals (nlines, nspans, nhuff, dst_need) are filled in on return, also on
  * QH_ERR_NOMEM (caps or dst_cap too small: nothing was decoded; resize and
  * call again).  opts: QH_SECTIONS_DTABLE0 decodes as a decoder whose

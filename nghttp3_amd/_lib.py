@@ -55,6 +55,8 @@ class qh_batch_stats(ctypes.Structure):
         ("out_bytes", ctypes.c_uint64),
         ("dst_bytes", ctypes.c_uint64),
         ("n_errors", ctypes.c_uint64),
+        ("lane_steps", ctypes.c_uint64),
+        ("wave_steps", ctypes.c_uint64),
     ]
 
 

@@ -108,6 +108,10 @@ struct DevStats {
   unsigned long long dst_bytes;
   unsigned long long n_errors;
   unsigned long long scan_timeouts;
+  // window decoders: lock-step iterations (16 table lookups each) run by
+  // lanes, and by waves (each wave's longest lane, per window)
+  unsigned long long lane_steps;
+  unsigned long long wave_steps;
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

@@ -19,8 +19,8 @@
 //   qh_k_scan, qh_k_synth_*   prefix sums, synthetic inputs (bench/tests)
 // Development variants (decoders fsm / fsm2 / lut / run / queue / other
 // peek widths and shapes, the chunk-engine and streaming encoders) build
-// only with
-// -DQH_DEV_VARIANTS (make dev -> libqhuff_dev.so).
+// only with -DQH_DEV_VARIANTS (make dev -> libqhuff_dev.so); the kernels
+// that exist only for them live outside the package, in dev/csrc (-I).
 
 #include <hip/hip_runtime.h>
 
@@ -47,7 +47,7 @@
 #include "qh_check.inc"       // field name / value checks (device)
 #include "qh_sched.inc"       // batch-wide length-class schedule (QH_DECODER_SORTED)
 #ifdef QH_DEV_VARIANTS         // development variants (make dev): not shipped
-#include "qh_lane_dec.inc"   // decoder: 4-bit FSM, one string per lane
+#include "qh_lane_dec.inc"   // (dev/csrc) decoder: 4-bit FSM, one string per lane
 #include "qh_lane_dec2.inc"  // decoder: 4-bit FSM, two strings per lane
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #endif

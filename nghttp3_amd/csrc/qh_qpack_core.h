@@ -68,6 +68,13 @@ typedef struct scan_out {
   size_t nhuff;    /* Huffman-coded strings seen */
   uint64_t hslots; /* their batch-decode slot bytes (include/qhuff.h) */
   uint32_t opts; /* QH_SECTIONS_DTABLE0: the decoder's table capacity is 0 */
+  /* (the GPU framing's write pass; zero elsewhere) lines name batch-global
+   * spans (span_base + the block's own index); every span's record goes to
+   * aux[] (block << 32 | its Huffman index, ~0u for a raw string) and every
+   * Huffman span also to huff[huff_base + its index among them] */
+  qh_span_in *huff;
+  uint64_t *aux;
+  uint64_t span_base, huff_base, block;
 } scan_out;
 
 /* One string literal: H bit at bit `prefix` of the first byte, then the
@@ -115,7 +122,13 @@ QH_HD static inline int read_string(scan_out *o, int32_t *span_idx, const uint8_
     s = &o->spans[o->nspans];
     *s = rec;
   }
-  *span_idx = (int32_t)o->nspans++;
+  if (o->aux) {
+    o->aux[o->nspans] = (o->block << 32) | (h ? (uint32_t)(o->huff_base + o->nhuff) : 0xFFFFFFFFu);
+  }
+  if (h && o->huff && o->spans) {
+    o->huff[o->huff_base + o->nhuff] = o->spans[o->nspans];
+  }
+  *span_idx = (int32_t)(o->span_base + o->nspans++);
   o->nhuff += h ? 1 : 0;
   /* the slot qh_decode_batch gives it: len * 8 / 5 + 16, rounded up to 64 */
   o->hslots += h ? ((len * 8 / 5 + 16 + 63) & ~(uint64_t)63) : 0;

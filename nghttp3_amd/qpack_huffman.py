@@ -168,15 +168,15 @@ class HuffmanBatchCodec:
 
     # -- context utilities --------------------------------------------------
     def set_decoder(self, kind: str):
-        """'windows' (default: strings of similar length) or 'waves' (skewed
-        lengths, e.g. Zipf up to 4 KiB); results are identical."""
+        """'sorted' (default: batch-wide length-class schedule), 'windows' or
+        'waves' (include/qhuff.h QH_DECODER_*); results are identical."""
         k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES,
              "sorted": _lib.QH_DECODER_SORTED}[kind]
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
 
     def set_encoder(self, kind: str):
-        """'windows' (default: strings of similar length) or 'waves' (skewed
-        or long strings); results are identical."""
+        """'windows' (default: strings of similar length), 'waves' or 'fused'
+        (one pass: long strings, binary text); results are identical."""
         k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES,
              "fused": _lib.QH_ENCODER_FUSED}[kind]
         _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")

@@ -575,7 +575,7 @@ def test_encode_dst_cap_too_small(codec, corpus):
 
 
 # The two shipped decoders (qh_ctx_set_decoder); the development variants
-# (make dev) are timed by scripts/dec_variants.py, not shipped.
+# (make dev) are timed by dev/scripts/dec_variants.py, not shipped.
 DECODERS = ["windows", "waves", "sorted"]
 # (development: QHUFF_LIB=nghttp3_amd/lib/libqhuff_dev.so QH_TEST_DEV_DECODERS=
 # peek11su,... adds those variants of the development build to these tests)

@@ -64,6 +64,18 @@ def _check_against_oracle(src, blocks, res, refdata, dtable0, strs_dst=None, src
         nbad += rst != 0
         k0, k1 = int(ss[b]), int(ss[b + 1])
         assert k1 - k0 == len(rspans), b
+        # lines: the oracle's for a clean block; none when the framing failed;
+        # all of them when only a Huffman string failed (-401 after a clean
+        # framing keeps its lines: include/qhuff.h qh_decode_sections_batch)
+        fst, _, flines, _ = ref.scan_field_section(data[off:off + n], off, dtable0)
+        l0, l1 = int(res["line_start"][b]), int(res["line_start"][b + 1])
+        got_lines = [(int(x["opcode"]), int(x["flags"]), int(x["index"]),
+                      int(x["name"]) - k0 if int(x["name"]) >= 0 else -1,
+                      int(x["value"]) - k0 if int(x["value"]) >= 0 else -1)
+                     for x in res["lines"][l0:l1]]
+        assert got_lines == (flines if fst == 0 else []), b
+        if rst == 0:
+            assert got_lines == rlines, b
         got_spans = [(int(x["off"]), int(x["len"]), int(x["flags"])) for x in res["spans"][k0:k1]]
         assert got_spans == rspans, b
         for j, k in enumerate(range(k0, k1)):
