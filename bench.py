@@ -277,6 +277,10 @@ def main():
     codec.enable_timing(False)
     t_dec = timed(lambda: codec.decode_dev(enc, eout, dec, dout), args.steps)
     t_enc = timed(lambda: codec.encode_dev(src, spans, enc, eout), args.steps)
+    # packed device output (QH_WHERE_DEVICE_DENSE: the slot decode, then a
+    # packing pass), reported beside the slot layout
+    t_dense = timed(lambda: codec.decode_dev(enc, eout, dec, dout, dense=True), args.steps)
+    dense_ok = D.sum(0.0 if roundtrip_ok(src, spans, dec, dout) else 1.0) == 0
     total_all = D.sum(float(total))
     value = total_all * args.steps / elapsed_max / GIB
 
@@ -446,6 +450,8 @@ def main():
             "cpu_baseline": cpu,
             "extra": {"decode_GiBps": round(total_all / t_dec / GIB, 2),
                       "encode_GiBps": round(total_all / t_enc / GIB, 2),
+                      "decode_dense_GiBps": round(total_all / t_dense / GIB, 2),
+                      "decode_dense_bit_exact": dense_ok,
                       "enc_global_offset_rank0": enc_global_off,
                       "kernels": kern, "host_path": host_path,
                       "config5_zipf": config5, "config4_qpack_blocks": config4,

@@ -9,7 +9,7 @@ from collections import defaultdict
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nghttp3_amd import HuffmanBatchCodec, _lib  # noqa: E402
 from nghttp3_amd.qpack_huffman import decode_slot_size  # noqa: E402
 from nghttp3_amd.synth import ALPHABET_A  # noqa: E402

@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("QHUFF_LIB", os.path.join(ROOT, "nghttp3_amd", "lib", "libqhuff_dev.so"))
 

@@ -9,7 +9,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nghttp3_amd import HuffmanBatchCodec, _lib, synth  # noqa: E402
 
 PHASES = {0: "head (tile, strings, scan)", 1: "chunks (load, lookups, scan)",

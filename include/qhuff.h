@@ -118,6 +118,11 @@ QH_EXPORT int nghttp3_qpack_huffman_decode_failure_state(
 /* Where the pointers handed to a batch call live. */
 #define QH_WHERE_HOST 0   /* host memory; the call copies H2D/D2H, blocks */
 #define QH_WHERE_DEVICE 1 /* HBM; the call is asynchronous on ctx stream */
+/* qh_decode_batch only: HBM, asynchronous, the decoded strings packed back
+ * to back in dst as with QH_WHERE_HOST (out[i].off = the decoded bytes
+ * before string i); the strings are decoded into a context scratch buffer of
+ * dst_cap bytes first, then packed (one more pass over the decoded bytes). */
+#define QH_WHERE_DEVICE_DENSE 2
 
 /* One string: bytes [off, off + len) of the batch's source buffer. */
 typedef struct qh_span_in {

@@ -23,6 +23,7 @@ QH_ERR_NOMEM = -901
 
 QH_WHERE_HOST = 0
 QH_WHERE_DEVICE = 1
+QH_WHERE_DEVICE_DENSE = 2
 QH_DECODER_WINDOWS = 0
 QH_DECODER_WAVES = 1
 QH_DECODER_SORTED = 2

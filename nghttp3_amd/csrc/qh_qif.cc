@@ -49,6 +49,24 @@
 
 #include "../../include/qhuff.h"
 
+
+namespace {
+// The text nghttp3_strerror gives these codes (lib/nghttp3_err.c:28-85),
+// which the reference CLI prints after a failed call.
+const char *qh_strerror(int rv) {
+  switch (rv) {
+  case QH_ERR_INVALID_ARGUMENT: return "ERR_INVALID_ARGUMENT";
+  case QH_ERR_QPACK_FATAL: return "ERR_QPACK_FATAL";
+  case QH_ERR_QPACK_HEADER_TOO_LARGE: return "ERR_QPACK_HEADER_TOO_LARGE";
+  case QH_ERR_QPACK_DECOMPRESSION_FAILED: return "ERR_QPACK_DECOMPRESSION_FAILED";
+  case QH_ERR_QPACK_ENCODER_STREAM_ERROR: return "ERR_QPACK_ENCODER_STREAM_ERROR";
+  case QH_ERR_NOMEM: return "ERR_NOMEM";
+  case QH_ERR_FATAL: return "ERR_FATAL";
+  default: return "(unknown)";
+  }
+}
+}  // namespace
+
 namespace {
 
 struct Config {
@@ -187,7 +205,7 @@ int encode(const char *outfile, const char *infile) {
       }
     }
     if (rv != 0) {
-      std::cerr << "encode: " << rv << std::endl;
+      std::cerr << "encode: " << qh_strerror(rv) << std::endl;
       return -1;
     }
     double t2 = now_ms();
@@ -476,7 +494,7 @@ int decode(const char *outfile, const char *infile) {
       const int rv = qh_decode_batch(ctx(), file.data(), huff.data(), nh, dst.data(), dst.size(),
                                      hout_batch.data(), QH_WHERE_HOST);
       if (rv != 0) {
-        std::cerr << "qh_decode_batch: " << rv << std::endl;
+        std::cerr << "qh_decode_batch: " << qh_strerror(rv) << std::endl;
         return -1;
       }
     }
@@ -502,15 +520,15 @@ int decode(const char *outfile, const char *infile) {
     if (!strings_ok(r)) {
       std::cerr << (r.stream_id == 0 ? "nghttp3_qpack_decoder_read_encoder: "
                                      : "nghttp3_qpack_decoder_read_request: ")
-                << (r.stream_id == 0 ? QH_ERR_QPACK_ENCODER_STREAM_ERROR
-                                     : QH_ERR_QPACK_DECOMPRESSION_FAILED)
+                << qh_strerror(r.stream_id == 0 ? QH_ERR_QPACK_ENCODER_STREAM_ERROR
+                                                : QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
       return -1;
     }
     if (r.rv != 0) {
       std::cerr << (r.stream_id == 0 ? "nghttp3_qpack_decoder_read_encoder: "
                                      : "nghttp3_qpack_decoder_read_request: ")
-                << r.rv << std::endl;
+                << qh_strerror(r.rv) << std::endl;
       return -1;
     }
     if (r.stream_id == 0) {
@@ -537,7 +555,7 @@ int decode(const char *outfile, const char *infile) {
                                              : table.add(ent.name, d.str((size_t)l.value));
         }
         if (!ok) {
-          std::cerr << "nghttp3_qpack_decoder_read_encoder: " << QH_ERR_QPACK_ENCODER_STREAM_ERROR
+          std::cerr << "nghttp3_qpack_decoder_read_encoder: " << qh_strerror(QH_ERR_QPACK_ENCODER_STREAM_ERROR)
                     << std::endl;
           return -1;
         }
@@ -546,7 +564,7 @@ int decode(const char *outfile, const char *infile) {
         const Blocked b = blocked.top();
         blocked.pop();
         if (!emit(table, recs[b.rec], b.ricnt, b.base, lines, d, out)) {
-          std::cerr << "nghttp3_qpack_decoder_read_request: " << QH_ERR_QPACK_DECOMPRESSION_FAILED
+          std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                     << std::endl;
           return -1;
         }
@@ -562,7 +580,7 @@ int decode(const char *outfile, const char *infile) {
       base = ricnt + r.prefix.delta_base;
     }
     if (!ok) {
-      std::cerr << "nghttp3_qpack_decoder_read_request: " << QH_ERR_QPACK_DECOMPRESSION_FAILED
+      std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
       return -1;
     }
@@ -575,7 +593,7 @@ int decode(const char *outfile, const char *infile) {
       continue;
     }
     if (!emit(table, r, ricnt, base, lines, d, out)) {
-      std::cerr << "nghttp3_qpack_decoder_read_request: " << QH_ERR_QPACK_DECOMPRESSION_FAILED
+      std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
       return -1;
     }

@@ -206,13 +206,16 @@ class HuffmanBatchCodec:
     def _ptr(t):
         return ctypes.c_void_p(t.data_ptr())
 
-    def decode_dev(self, src, spans, dst, out):
+    def decode_dev(self, src, spans, dst, out, dense: bool = False):
         """src: uint8 [>=extent], spans: int64 [n,2], dst: uint8 [cap],
-        out: int64 [n,2].  Asynchronous on the context stream."""
+        out: int64 [n,2].  Asynchronous on the context stream.  dense: the
+        decoded strings packed back to back (QH_WHERE_DEVICE_DENSE) instead
+        of the slot layout."""
         n = spans.shape[0]
         _lib.check(self._lib.qh_decode_batch(self._ctx, self._ptr(src), self._ptr(spans), n,
                                              self._ptr(dst), dst.numel(), self._ptr(out),
-                                             QH_WHERE_DEVICE), "qh_decode_batch")
+                                             _lib.QH_WHERE_DEVICE_DENSE if dense else QH_WHERE_DEVICE),
+                   "qh_decode_batch")
 
     def encode_count_dev(self, src, spans, hlen):
         n = spans.shape[0]

@@ -101,6 +101,35 @@ def test_corpus_decode(codec, corpus):
         assert dst[o[i]:o[i] + l[i]].tobytes() == plain[off[i]:off[i] + ln[i]].tobytes(), i
 
 
+@pytest.mark.parametrize("kind", ["good", "corrupted"])
+def test_dense_device_output(codec, corpus, kind):
+    """QH_WHERE_DEVICE_DENSE: the decoded strings packed back to back in HBM
+    (out[i].off = the decoded bytes of the successful strings before i),
+    the same bytes, lengths and statuses as the oracle, on the corpus and on
+    the corrupted strings (failed strings take no bytes)."""
+    torch = torch_mod()
+    if kind == "good":
+        enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    else:
+        enc, eoff, elen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+    want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
+    n = len(elen)
+    cap = int(q.decode_slot_size(elen.astype(np.int64)).sum())
+    dst = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(to_dev(enc), spans_dev(eoff, elen), dst, out, dense=True)
+    o, l, s = q.unpack_out(out)
+    d = dst.cpu().numpy()
+    assert (s == want_st.astype(np.int64)).all()
+    ok = s == 0
+    assert (l[ok] == want_len[ok].astype(np.int64)).all()
+    lens = np.where(ok, l, 0)
+    assert (o == np.concatenate([[0], np.cumsum(lens)[:-1]])).all()
+    for i in np.nonzero(ok)[0]:
+        w = want_dst[int(want_slot[i]):int(want_slot[i]) + int(want_len[i])]
+        assert d[o[i]:o[i] + l[i]].tobytes() == w.tobytes(), i
+
+
 def test_corpus_encode(codec, corpus):
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
     enc, o, l, s = encode_dev(codec, plain, off, ln)

@@ -179,6 +179,8 @@ def test_sections_pipeline_matches_oracle_on_corrupted_blocks(dec, dec0, refdata
             "strs": g["strs"][:ns].cpu().numpy().view(qpack.SPAN_OUT_DTYPE).reshape(-1),
             "verdict": g["verdict"][:ns].cpu().numpy(), "tokens": g["tokens"][:ns].cpu().numpy(),
             "span_start": g["span_start"][:blocks.size + 1].cpu().numpy().view(np.uint32),
+            "line_start": g["line_start"][:blocks.size + 1].cpu().numpy().view(np.uint32),
+            "lines": g["lines"][:int(g["nlines"]) * 24].cpu().numpy().view(qpack.FIELD_LINE_DTYPE),
             "status": g["status"][:blocks.size].cpu().numpy(), "dst": g["dst"].cpu().numpy()}
     assert (gres["status"] == res["status"]).all()
     _check_against_oracle(src, blocks, gres, refdata, dtable0)
