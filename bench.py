@@ -150,14 +150,14 @@ def lds_secondary(kernel, avg_us, n, args):
         return None
     if st["strings"] != n:
         return None
-    lookups = st["sorted"]["lookups"]
+    lookups = st["windows"]["lookups"]
     rate = lookups / (avg_us * 1e-6)
     agg = LDS_B32_TBPS * 1e12 / 4
     return {"unit": "lookups/s", "lookups_per_launch": lookups, "achieved": round(rate, -6),
             "chained_rate": chain["chained_lookups_per_s_best"],
             "frac_of_chained_rate": round(rate / chain["chained_lookups_per_s_best"], 4),
             "ds_read_b32_aggregate": agg, "frac_of_aggregate": round(rate / agg, 4),
-            "active_lane_frac": st["sorted"]["active_lane_frac"],
+            "active_lane_frac": st["windows"]["active_lane_frac"],
             "source": "profiles/r03/decoder_steps.json (make stamps, QH_STEP_COUNTS), "
                       "profiles/r03/lds_chain.json"}
 
@@ -363,6 +363,7 @@ def main():
         k5 = kernel_table(codec.kernel_times(), sp5.shape[0], tot5, eb5)
         codec.enable_timing(False)
         codec.set_encoder("windows")
+        codec.set_decoder("windows")
         d5 = k5.get("qh_k_dec_peek", {})
         p5, e5 = D.sum(float(tot5)), D.sum(float(eb5))
         dec_gbps_min = D.max(-d5.get("achieved_GBps", 0.0))
@@ -371,7 +372,7 @@ def main():
                               "mean %.1f B" % float(ln5.mean()),
                    "shards": world, "strings_rank0": int(c1 - c0) if rank == 0 else None,
                    "encode_GiBps": round(p5 / te5 / GIB, 2), "decode_GiBps": round(p5 / td5 / GIB, 2),
-                   "decoder": "sorted (default: length-class schedule + qh_k_dec_peek windows)",
+                   "decoder": "sorted (QH_DECODER_SORTED: length-class schedule + qh_k_dec_peek windows)",
                    "decode_GiBps_wave_decoder": round(p5 / D.max(td5_alt) / GIB, 2),
                    "encoder": "fused (qh_k_encw: lengths and codes in one pass over the plaintext)",
                    "encode_GiBps_window_encoder": round(p5 / D.max(te5_alt) / GIB, 2),
@@ -399,18 +400,22 @@ def main():
         u_src, u_spans, u_total = codec.synth(args.seed, args.strings, args.min_len, args.max_len, synth.ALPHABET_U)
         u_enc, u_eout, u_eb, u_dec, u_dout = buffers(u_src, u_spans)
         tue_win = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 3)
-        codec.set_encoder("fused")  # (binary text: the one-pass encoder)
+        codec.set_encoder("fused")  # (binary text: the one-pass encoder, the sorted decoder)
+        codec.set_decoder("sorted")
         u_enc.zero_()
         codec.encode_dev(u_src, u_spans, u_enc, u_eout)
         codec.decode_dev(u_enc, u_eout, u_dec, u_dout)
         u_ok = roundtrip_ok(u_src, u_spans, u_dec, u_dout)
         tue = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 5)
         tud = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 5)
+        codec.set_decoder("windows")
+        tud_win = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 3)
         codec.set_encoder("windows")
         configU = {"strings": args.strings, "plain_bytes": u_total, "enc_bytes": u_eb,
                    "encode_GiBps": round(u_total / tue / GIB, 2), "encoder": "fused",
                    "encode_GiBps_window_encoder": round(u_total / tue_win / GIB, 2),
-                   "decode_GiBps": round(u_total / tud / GIB, 2), "decoder": "sorted (default)",
+                   "decode_GiBps": round(u_total / tud / GIB, 2), "decoder": "sorted",
+                   "decode_GiBps_window_decoder": round(u_total / tud_win / GIB, 2),
                    "round_trip_GiBps": round(u_total / (tue + tud) / GIB, 2), "bit_exact": u_ok}
         del u_src, u_spans, u_enc, u_eout, u_dec, u_dout
 

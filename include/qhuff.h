@@ -168,17 +168,21 @@ QH_EXPORT int qh_ctx_new(qh_ctx **pctx, int device, void *stream);
 QH_EXPORT void qh_ctx_del(qh_ctx *ctx);
 QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
 /* Decoder kernel of qh_decode_batch (results are identical; speed is not):
- * QH_DECODER_WINDOWS sorts each 256-string window by length and decodes a
- * window per workgroup; QH_DECODER_WAVES lets every wave sort and decode its
- * own chunks of 256 strings with no workgroup barrier, its input staged
- * through LDS in 64-byte groups. */
+ * QH_DECODER_WINDOWS (default) sorts each 256-string window by length and
+ * decodes a window per workgroup -- fastest for header strings of similar
+ * length (8-256 B, and the 1-128 B strings of whole field sections);
+ * QH_DECODER_WAVES lets every wave sort and decode its own chunks of 256
+ * strings with no workgroup barrier, its input staged through LDS in
+ * 64-byte groups. */
 #define QH_DECODER_WINDOWS 0
 #define QH_DECODER_WAVES 1
-/* QH_DECODER_SORTED (default): the window decoder over a batch-wide
- * schedule -- passes over the spans sort the strings into 16-byte length
+/* QH_DECODER_SORTED: the window decoder over a batch-wide schedule --
+ * three short passes over the spans sort the strings into 16-byte length
  * classes, longest first, so every 256-string window holds strings of one
- * class (same output layout).  On one MI355X: 8-256 B headers as fast as
- * QH_DECODER_WINDOWS, binary text 1.3x, Zipf lengths to 4 KiB 4.6x. */
+ * class (same output layout).  For skewed lengths and binary text: on one
+ * MI355X, Zipf lengths to 4 KiB decode 2.3x the wave decoder and 6x the
+ * window decoder, binary text 1.3x; 8-256 B headers ~5% slower than
+ * QH_DECODER_WINDOWS (the schedule's ~25 us). */
 #define QH_DECODER_SORTED 2
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 /* Codes kernel of qh_encode_batch (results are identical; speed is not):

@@ -168,8 +168,9 @@ class HuffmanBatchCodec:
 
     # -- context utilities --------------------------------------------------
     def set_decoder(self, kind: str):
-        """'sorted' (default: batch-wide length-class schedule), 'windows' or
-        'waves' (include/qhuff.h QH_DECODER_*); results are identical."""
+        """'windows' (default), 'sorted' (batch-wide length-class schedule:
+        skewed lengths, binary text) or 'waves' (include/qhuff.h
+        QH_DECODER_*); results are identical."""
         k = {"windows": _lib.QH_DECODER_WINDOWS, "waves": _lib.QH_DECODER_WAVES,
              "sorted": _lib.QH_DECODER_SORTED}[kind]
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
