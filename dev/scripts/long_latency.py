@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Decode time of a few long strings (the wave-per-string path of the sorted
+decoder against the lane path), and of rank 0's config-5 shard at several
+thresholds (development tool, one GPU).  QHUFF_LONG_MIN is read at context
+creation, so each setting gets its own context."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def run(lmin, src, spans, total, label, reps=5):
+    import torch
+    from nghttp3_amd import HuffmanBatchCodec
+    from nghttp3_amd.qpack_huffman import decode_slot_size
+    os.environ["QHUFF_LONG_MIN"] = str(lmin)
+    c = HuffmanBatchCodec(device=0)
+    c.set_decoder("sorted")
+    n = spans.shape[0]
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()) + 64, dtype=torch.uint8, device="cuda")
+    eout = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    c.encode_dev(src, spans, enc, eout)
+    cap = int(decode_slot_size(eout[:, 1] & 0xFFFFFFFF).sum().item())
+    dec = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    dout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    c.decode_dev(enc, eout, dec, dout)
+    st = c.stats()
+    ok = st["n_errors"] == 0 and st["out_bytes"] == total
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        c.decode_dev(enc, eout, dec, dout)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    print(json.dumps({"case": label, "long_min": lmin, "strings": n, "plain_bytes": total, "decode_us": round(us, 1),
+                      "GiBps": round(total / (us * 1e-6) / 2**30, 1), "ok": ok}), flush=True)
+    c.close()
+
+
+def main():
+    import numpy as np
+    import torch
+    from nghttp3_amd import HuffmanBatchCodec, synth
+    base = HuffmanBatchCodec(device=0)
+    for nstr, ln in ((1, 65536), (64, 65536), (1024, 8192)):
+        spans, total = base.spans_to_device(np.full(nstr, ln, dtype=np.int64))
+        src = base.synth_fill(0x5EED0007, 0, total, synth.ALPHABET_A)
+        for lmin in (4096, 0):
+            run(lmin, src, spans, total, f"{nstr} x {ln} B")
+    zl = synth.zipf_lengths(0x5EED0005, 2097152, 1, 4096, 1.2)
+    spans, total = base.spans_to_device(zl)
+    src = base.synth_fill(0x5EED0005, 0, total, synth.ALPHABET_A)
+    for lmin in (0, 4096, 2048):
+        run(lmin, src, spans, total, "config-5 shard")
+
+
+if __name__ == "__main__":
+    main()

@@ -749,6 +749,71 @@ def test_long_code_mode_matches_oracle(kind):
         c.close()
 
 
+def _long_strings(rng, n_ok, alphabet, lo, hi):
+    """n_ok strings of lo..hi plaintext bytes over `alphabet`, oracle-encoded,
+    plus corrupted copies of some of them (a bit flipped, EOS appended,
+    the last byte dropped, padding zeroed)."""
+    alph = np.frombuffer(alphabet, dtype=np.uint8)
+    plains = [bytes(alph[rng.integers(0, alph.size, int(rng.integers(lo, hi + 1)))]) for _ in range(n_ok)]
+    src, sp = q.pack_strings(plains)
+    enc, eoff, elen = oracle.encode_batch(src, sp["off"], sp["len"])
+    strs = [bytes(enc[int(o):int(o) + int(l)]) for o, l in zip(eoff, elen)]
+    bad = []
+    for k, e in enumerate(strs[: n_ok // 2]):
+        b = bytearray(e)
+        kind = k % 4
+        if kind == 0:
+            b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 1:
+            b += b"\xff\xff\xff\xfc"  # EOS (30 ones) and more
+        elif kind == 2:
+            b = b[:-1] + b"\x00"
+        else:
+            b[-1] &= 0xF0
+        bad.append(bytes(b))
+    return strs + bad
+
+
+@pytest.mark.parametrize("alphabet", ["A", "U"])
+def test_long_strings_wave_per_string(alphabet):
+    """The sorted decoder's wave-per-string path (strings of its longest
+    class, qh_peek_dec.inc pk_long_string: lanes start at 16-byte
+    boundaries and resynchronise) on strings of 4-40 KB, and on strings of
+    200-3000 B with the threshold lowered (QHUFF_LONG_MIN) so that both
+    paths run in one batch: statuses, lengths and bytes as the oracle's."""
+    from nghttp3_amd import HuffmanBatchCodec
+    rng = np.random.default_rng(0x10A9 + (alphabet == "U"))
+    alph = synth.ALPHABET_A if alphabet == "A" else synth.ALPHABET_U
+    cases = [(None, _long_strings(rng, 96, alph, 4096, 40000)),
+             ("300", _long_strings(rng, 600, alph, 200, 3000) + _long_strings(rng, 40, alph, 1, 64))]
+    for long_min, strs in cases:
+        old = os.environ.get("QHUFF_LONG_MIN")
+        if long_min is not None:
+            os.environ["QHUFF_LONG_MIN"] = long_min
+        try:
+            c = HuffmanBatchCodec(device=0)
+        finally:
+            if old is None:
+                os.environ.pop("QHUFF_LONG_MIN", None)
+            else:
+                os.environ["QHUFF_LONG_MIN"] = old
+        try:
+            c.set_decoder("sorted")
+            order = rng.permutation(len(strs))
+            strs = [strs[i] for i in order]
+            src, sp = q.pack_strings(strs)
+            want_dst, want_slot, want_len, want_st = oracle.decode_batch(src, sp["off"], sp["len"])
+            assert (want_st != 0).sum() > 10 and (want_st == 0).sum() > 40
+            dst, o, l, s = decode_dev(c, src, sp["off"], sp["len"])
+            assert (s == want_st.astype(np.int64)).all()
+            assert (l == want_len.astype(np.int64)).all()
+            for j in np.nonzero(s == 0)[0]:
+                ws = int(want_slot[j])
+                assert dst[o[j]:o[j] + l[j]].tobytes() == want_dst[ws:ws + int(want_len[j])].tobytes(), j
+        finally:
+            c.close()
+
+
 @pytest.mark.parametrize("mode", ["default", "lane"])
 def test_encode_length_passes(mode, corpus, digests):
     """The encoder's passes: streaming lengths + lane-per-string codes
