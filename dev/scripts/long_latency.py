@@ -10,13 +10,13 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
-def run(lmin, src, spans, total, label, reps=5):
+def run(lmin, src, spans, total, label, reps=5, decoder="sorted"):
     import torch
     from nghttp3_amd import HuffmanBatchCodec
     from nghttp3_amd.qpack_huffman import decode_slot_size
     os.environ["QHUFF_LONG_MIN"] = str(lmin)
     c = HuffmanBatchCodec(device=0)
-    c.set_decoder("sorted")
+    c.set_decoder(decoder)
     n = spans.shape[0]
     ln = spans[:, 1] & 0xFFFFFFFF
     enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()) + 64, dtype=torch.uint8, device="cuda")
@@ -36,7 +36,7 @@ def run(lmin, src, spans, total, label, reps=5):
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    print(json.dumps({"case": label, "long_min": lmin, "strings": n, "plain_bytes": total, "decode_us": round(us, 1),
+    print(json.dumps({"case": label, "decoder": decoder, "long_min": lmin, "strings": n, "plain_bytes": total, "decode_us": round(us, 1),
                       "GiBps": round(total / (us * 1e-6) / 2**30, 1), "ok": ok}), flush=True)
     c.close()
 
@@ -51,6 +51,7 @@ def main():
         src = base.synth_fill(0x5EED0007, 0, total, synth.ALPHABET_A)
         for lmin in (4096, 0):
             run(lmin, src, spans, total, f"{nstr} x {ln} B")
+        run(4096, src, spans, total, f"{nstr} x {ln} B", decoder="windows")
     zl = synth.zipf_lengths(0x5EED0005, 2097152, 1, 4096, 1.2)
     spans, total = base.spans_to_device(zl)
     src = base.synth_fill(0x5EED0005, 0, total, synth.ALPHABET_A)

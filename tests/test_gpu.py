@@ -774,13 +774,15 @@ def _long_strings(rng, n_ok, alphabet, lo, hi):
     return strs + bad
 
 
+@pytest.mark.parametrize("decoder", ["sorted", "windows"])
 @pytest.mark.parametrize("alphabet", ["A", "U"])
-def test_long_strings_wave_per_string(alphabet):
-    """The sorted decoder's wave-per-string path (strings of its longest
-    class, qh_peek_dec.inc pk_long_string: lanes start at 16-byte
-    boundaries and resynchronise) on strings of 4-40 KB, and on strings of
-    200-3000 B with the threshold lowered (QHUFF_LONG_MIN) so that both
-    paths run in one batch: statuses, lengths and bytes as the oracle's."""
+def test_long_strings_wave_per_string(alphabet, decoder):
+    """The wave-per-string path (qh_peek_dec.inc pk_long_string: lanes
+    start at 16-byte boundaries and resynchronise) on strings of 4-40 KB --
+    the sorted decoder's longest class, the window decoder's deferred
+    strings -- and on strings of 200-3000 B with the sorted decoder's
+    threshold lowered (QHUFF_LONG_MIN) so that both paths run in one batch:
+    statuses, lengths and bytes as the oracle's."""
     from nghttp3_amd import HuffmanBatchCodec
     rng = np.random.default_rng(0x10A9 + (alphabet == "U"))
     alph = synth.ALPHABET_A if alphabet == "A" else synth.ALPHABET_U
@@ -798,7 +800,7 @@ def test_long_strings_wave_per_string(alphabet):
             else:
                 os.environ["QHUFF_LONG_MIN"] = old
         try:
-            c.set_decoder("sorted")
+            c.set_decoder(decoder)
             order = rng.permutation(len(strs))
             strs = [strs[i] for i in order]
             src, sp = q.pack_strings(strs)
