@@ -426,12 +426,48 @@ int decode(const char *outfile, const char *infile) {
     recs.push_back(r);
     p += size;
   }
+  // An encoder instruction cut by the end of a stream-0 record continues in
+  // the next stream-0 record, as the reference decoder keeps the partial
+  // instruction's state between read_encoder calls (qpack.c:2815-3150): its
+  // bytes move to the front of the next stream-0 record (a new region
+  // appended to the file), where the instruction completes and takes effect;
+  // a partial instruction at the end of the file is left pending, as there.
+  {
+    std::vector<qh_field_line> tl(n + 1);
+    std::vector<qh_span_in> ts(n + 1);
+    std::vector<uint8_t> tail;
+    size_t extra = 0;
+    for (auto &r : recs)
+      if (r.stream_id == 0) extra += r.len;
+    file.reserve(file.size() + 2 * extra + 1);
+    for (auto &r : recs) {
+      if (r.stream_id != 0) continue;
+      if (!tail.empty()) {  // this record, behind the previous one's tail
+        tail.insert(tail.end(), file.begin() + (std::ptrdiff_t)r.off,
+                    file.begin() + (std::ptrdiff_t)(r.off + r.len));
+        r.off = file.size();
+        r.len = tail.size();
+        file.insert(file.end(), tail.begin(), tail.end());
+        tail.clear();
+      }
+      size_t nl = 0, ns = 0;
+      const nghttp3_ssize done = qh_qpack_scan_encoder_stream(file.data() + r.off, r.len, r.off,
+                                                              tl.data(), tl.size(), &nl, ts.data(),
+                                                              ts.size(), &ns);
+      if (done >= 0 && (size_t)done < r.len) {
+        tail.assign(file.begin() + (std::ptrdiff_t)(r.off + (size_t)done),
+                    file.begin() + (std::ptrdiff_t)(r.off + r.len));
+        r.len = (size_t)done;
+      }
+    }
+  }
+  const size_t nf = file.size();
   if (file.empty()) file.push_back(0);
-  std::vector<qh_field_line> lines(n + 1);
-  std::vector<qh_span_in> spans(n + 1);
+  std::vector<qh_field_line> lines(nf + 1);
+  std::vector<qh_span_in> spans(nf + 1);
   std::vector<qh_span_in> huff;
   std::vector<size_t> huff_of;  // Huffman string j -> span index
-  std::vector<qh_span_out> hout_batch, hout(n + 1);
+  std::vector<qh_span_out> hout_batch, hout(nf + 1);
   std::vector<uint8_t> dst;
   std::vector<double> t_frame, t_batch;
   const int reps = config.time_reps > 0 ? config.time_reps : 1;

@@ -116,6 +116,31 @@ def test_driver_scalar_decodes_corpus(tmp_path):
     assert out == open(NETBSD_QIF, "rb").read()
 
 
+def test_driver_scalar_carries_partial_encoder_instructions(tmp_path):
+    """Every encoder-stream record cut in two records at its middle byte (an
+    instruction split across them): the decoder keeps the partial
+    instruction until the next encoder-stream record completes it, as the
+    reference's read_encoder does; the QIF is the corpus's."""
+    import struct
+    data = open(CORPUS, "rb").read()
+    recs = qf.read_qif_out(data)
+    out = []
+    nsplit = 0
+    for sid, off, n in recs:
+        body = data[off:off + n]
+        if sid == 0 and n >= 2:
+            h = n // 2
+            out.append(struct.pack(">QI", 0, h) + body[:h])
+            out.append(struct.pack(">QI", 0, n - h) + body[h:])
+            nsplit += 1
+        else:
+            out.append(data[off - 12:off + n])
+    assert nsplit > 0
+    r, got = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], b"".join(out))
+    assert r.returncode == 0, r.stderr
+    assert got == open(NETBSD_QIF, "rb").read()
+
+
 def test_driver_scalar_releases_blocked_streams(tmp_path):
     """Each request record moved before the encoder-stream record that
     precedes it: the decoder blocks it (Required Insert Count > inserts so
