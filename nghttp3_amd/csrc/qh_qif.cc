@@ -487,6 +487,7 @@ int decode(const char *outfile, const char *infile) {
             spans.data() + ns_tot, spans.size() - ns_tot, &ns);
         r.rv = rv < 0 ? (int)rv : ((size_t)rv != r.len ? QH_ERR_QPACK_ENCODER_STREAM_ERROR : 0);
       } else {
+        r.prefix.reserved = 0xFFFFFFFFu;  // (the parser sets it to 0 once the prefix is read)
         r.rv = qh_qpack_scan_field_section(file.data() + r.off, r.len, r.off, &r.prefix,
                                            lines.data() + nl_tot, lines.size() - nl_tot, &nl,
                                            spans.data() + ns_tot, spans.size() - ns_tot, &ns);
@@ -551,22 +552,32 @@ int decode(const char *outfile, const char *infile) {
       if ((spans[k].flags & QH_SPAN_HUFFMAN) && hout[k].status != 0) return false;
     return true;
   };
-  for (size_t ri = 0; ri < recs.size(); ++ri) {
-    const Record &r = recs[ri];
+  // a record's Huffman and framing verdicts, reported as read_encoder /
+  // read_request would (a request's once it is not blocked)
+  auto record_ok = [&](const Record &r) {
     if (!strings_ok(r)) {
       std::cerr << (r.stream_id == 0 ? "nghttp3_qpack_decoder_read_encoder: "
                                      : "nghttp3_qpack_decoder_read_request: ")
                 << qh_strerror(r.stream_id == 0 ? QH_ERR_QPACK_ENCODER_STREAM_ERROR
                                                 : QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
-      return -1;
+      return false;
     }
     if (r.rv != 0) {
       std::cerr << (r.stream_id == 0 ? "nghttp3_qpack_decoder_read_encoder: "
                                      : "nghttp3_qpack_decoder_read_request: ")
                 << qh_strerror(r.rv) << std::endl;
-      return -1;
+      return false;
     }
+    return true;
+  };
+  for (size_t ri = 0; ri < recs.size(); ++ri) {
+    const Record &r = recs[ri];
+    // a request whose prefix was read blocks (or not) before its
+    // representations are decoded (qpack.c:3419-3436): its other verdicts
+    // come when it is emitted
+    const bool prefix_read = r.stream_id != 0 && r.prefix.reserved == 0;
+    if (!prefix_read && !record_ok(r)) return -1;
     if (r.stream_id == 0) {
       for (size_t i = r.line0; i < r.line0 + r.nline; ++i) {
         const qh_field_line &l = lines[i];
@@ -599,6 +610,7 @@ int decode(const char *outfile, const char *infile) {
       while (!blocked.empty() && blocked.top().ricnt <= table.icnt()) {
         const Blocked b = blocked.top();
         blocked.pop();
+        if (!record_ok(recs[b.rec])) return -1;
         if (!emit(table, recs[b.rec], b.ricnt, b.base, lines, d, out)) {
           std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                     << std::endl;
@@ -628,6 +640,7 @@ int decode(const char *outfile, const char *infile) {
       blocked.push({ricnt, seq++, base, ri});
       continue;
     }
+    if (!record_ok(r)) return -1;
     if (!emit(table, r, ricnt, base, lines, d, out)) {
       std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;

@@ -141,6 +141,35 @@ def test_driver_scalar_carries_partial_encoder_instructions(tmp_path):
     assert got == open(NETBSD_QIF, "rb").read()
 
 
+def test_driver_scalar_blocks_before_decoding(tmp_path):
+    """A request record with a bad Huffman string, moved ahead of the
+    encoder-stream record before it: the reference decoder reads the
+    section prefix, blocks the stream (Required Insert Count > inserts so
+    far) and only decodes the representations when it is unblocked, so at
+    -m 0 the error is the blocking one, and at -m 100 the Huffman one
+    (DECOMPRESSION_FAILED) once the inserts arrive."""
+    data = open(CORPUS, "rb").read()
+    recs = qf.read_qif_out(data)
+    raw = [bytearray(data[off - 12:off + n]) for _, off, n in recs]
+    sids = [sid for sid, _, _ in recs]
+    for k in range(1, len(raw)):
+        if sids[k] != 0 and sids[k - 1] == 0:
+            st, _, _, spans = qf.scan_field_section(bytes(raw[k][12:]), 0)
+            hs = [sp for sp in spans if sp[2] & qf.SPAN_HUFFMAN]
+            if st == 0 and hs:
+                o, n, _ = hs[0]
+                raw[k][12 + o + n - 1] = 0x00  # zero padding: an invalid string
+                raw[k - 1], raw[k] = raw[k], raw[k - 1]
+                break
+    else:
+        pytest.fail("no request record after an encoder-stream record")
+    wire = b"".join(bytes(x) for x in raw)
+    r, _ = _run(tmp_path, ["--scalar", "-s", "256", "-m", "0", "decode"], wire, "m0")
+    assert r.returncode != 0 and "blocked" in r.stderr and "DECOMPRESSION" not in r.stderr
+    r, _ = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], wire, "m100")
+    assert r.returncode != 0 and "ERR_QPACK_DECOMPRESSION_FAILED" in r.stderr
+
+
 def test_driver_scalar_releases_blocked_streams(tmp_path):
     """Each request record moved before the encoder-stream record that
     precedes it: the decoder blocks it (Required Insert Count > inserts so
