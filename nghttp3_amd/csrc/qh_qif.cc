@@ -552,6 +552,17 @@ int decode(const char *outfile, const char *infile) {
       if ((spans[k].flags & QH_SPAN_HUFFMAN) && hout[k].status != 0) return false;
     return true;
   };
+  // the output is written as the reference's streams it: what was emitted
+  // before an error stays in the file
+  std::ofstream of(outfile, std::ios::trunc | std::ios::binary);
+  if (!of) {
+    std::cerr << "Could not open file " << outfile << ": " << strerror(errno) << std::endl;
+    return -1;
+  }
+  auto fail_out = [&]() {
+    of.write(out.data(), (std::streamsize)out.size());
+    return -1;
+  };
   // a record's Huffman and framing verdicts, reported as read_encoder /
   // read_request would (a request's once it is not blocked)
   auto record_ok = [&](const Record &r) {
@@ -577,7 +588,7 @@ int decode(const char *outfile, const char *infile) {
     // representations are decoded (qpack.c:3419-3436): its other verdicts
     // come when it is emitted
     const bool prefix_read = r.stream_id != 0 && r.prefix.reserved == 0;
-    if (!prefix_read && !record_ok(r)) return -1;
+    if (!prefix_read && !record_ok(r)) return fail_out();
     if (r.stream_id == 0) {
       for (size_t i = r.line0; i < r.line0 + r.nline; ++i) {
         const qh_field_line &l = lines[i];
@@ -604,17 +615,17 @@ int decode(const char *outfile, const char *infile) {
         if (!ok) {
           std::cerr << "nghttp3_qpack_decoder_read_encoder: " << qh_strerror(QH_ERR_QPACK_ENCODER_STREAM_ERROR)
                     << std::endl;
-          return -1;
+          return fail_out();
         }
       }
       while (!blocked.empty() && blocked.top().ricnt <= table.icnt()) {
         const Blocked b = blocked.top();
         blocked.pop();
-        if (!record_ok(recs[b.rec])) return -1;
+        if (!record_ok(recs[b.rec])) return fail_out();
         if (!emit(table, recs[b.rec], b.ricnt, b.base, lines, d, out)) {
           std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                     << std::endl;
-          return -1;
+          return fail_out();
         }
       }
       continue;
@@ -630,29 +641,24 @@ int decode(const char *outfile, const char *infile) {
     if (!ok) {
       std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
-      return -1;
+      return fail_out();
     }
     if (ricnt > table.icnt()) {
       if (blocked.size() >= config.max_blocked) {
         std::cerr << "Too many blocked streams: max_blocked=" << config.max_blocked << std::endl;
-        return -1;
+        return fail_out();
       }
       blocked.push({ricnt, seq++, base, ri});
       continue;
     }
-    if (!record_ok(r)) return -1;
+    if (!record_ok(r)) return fail_out();
     if (!emit(table, r, ricnt, base, lines, d, out)) {
       std::cerr << "nghttp3_qpack_decoder_read_request: " << qh_strerror(QH_ERR_QPACK_DECOMPRESSION_FAILED)
                 << std::endl;
-      return -1;
+      return fail_out();
     }
   }
   double t4 = now_ms();
-  std::ofstream of(outfile, std::ios::trunc | std::ios::binary);
-  if (!of) {
-    std::cerr << "Could not open file " << outfile << ": " << strerror(errno) << std::endl;
-    return -1;
-  }
   of.write(out.data(), (std::streamsize)out.size());
   if (!blocked.empty()) {
     std::cerr << "Still " << blocked.size() << " stream(s) blocked" << std::endl;
