@@ -130,6 +130,48 @@ def test_dense_device_output(codec, corpus, kind):
         assert d[o[i]:o[i] + l[i]].tobytes() == w.tobytes(), i
 
 
+def test_dense_device_output_cap_and_sorted(codec, corpus):
+    """QH_WHERE_DEVICE_DENSE with dst_cap cut to half the decoded bytes:
+    strings that fit keep their packed place and bytes, the first that does
+    not and every later one get QH_ERR_NOMEM (nothing written past dst_cap);
+    and with the sorted decoder the packed output is the window decoder's."""
+    torch = torch_mod()
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    want_dst, want_slot, want_len, want_st = oracle.decode_batch(enc, eoff, elen)
+    n = len(elen)
+    total = int(want_len.astype(np.int64).sum())
+    cap = total // 2
+    dst = torch.full((cap + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(to_dev(enc), spans_dev(eoff, elen), dst[:cap], out, dense=True)
+    o, l, s = q.unpack_out(out)
+    d = dst.cpu().numpy()
+    assert (d[cap:] == 0xAB).all()
+    # (the slot-layout decode runs in a scratch of dst_cap bytes: the strings
+    # whose slots end within it succeed -- a prefix of the batch -- and pack
+    # into dst; every later one is QH_ERR_NOMEM)
+    k = int(np.argmax(s != 0)) if (s != 0).any() else n
+    assert 0 < k < n and (s[:k] == 0).all() and (s[k:] == q.QH_ERR_NOMEM).all()
+    lens = want_len[:k].astype(np.int64)
+    assert (l[:k] == lens).all() and (o[:k] == np.concatenate([[0], np.cumsum(lens)[:-1]])).all()
+    assert int(lens.sum()) <= cap
+    for j in range(0, k, max(1, k // 500)):
+        ws = int(want_slot[j])
+        assert d[o[j]:o[j] + l[j]].tobytes() == want_dst[ws:ws + int(want_len[j])].tobytes(), j
+    # the sorted decoder, full cap: the same packed bytes and spans
+    full = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    out_w = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(to_dev(enc), spans_dev(eoff, elen), full, out_w, dense=True)
+    ref = (full[:total].cpu().numpy().copy(), out_w.cpu().numpy().copy())
+    codec.set_decoder("sorted")
+    try:
+        full.zero_()
+        codec.decode_dev(to_dev(enc), spans_dev(eoff, elen), full, out_w, dense=True)
+        assert (full[:total].cpu().numpy() == ref[0]).all() and (out_w.cpu().numpy() == ref[1]).all()
+    finally:
+        codec.set_decoder("windows")
+
+
 def test_corpus_encode(codec, corpus):
     plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
     enc, o, l, s = encode_dev(codec, plain, off, ln)
