@@ -119,6 +119,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // unaligned addresses (unaligned access mode), so a string can be fetched
 // from its own first byte without a head-alignment loop.
 typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+typedef uint64_t u64_ua __attribute__((aligned(1)));
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+typedef uint16_t u16_ua __attribute__((aligned(1)));
 
 // Host images of the tables uploaded to every context (qh_tables.h lists).
 #define QH_SYM_PAIR(nbits, code) nbits, code,
