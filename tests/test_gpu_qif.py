@@ -52,15 +52,38 @@ def test_encode_sections_matches_host_writer(enc):
         assert sec == head + body
 
 
-@pytest.mark.parametrize("nsec", [1, 2047, 2048, 2049, 4097])
+@pytest.mark.parametrize("nsec", [1, 3, 4, 5, 63, 64, 65, 2047, 2048, 2049, 4097])
 def test_encode_sections_at_scan_tile_edges(enc, nsec):
-    """The section sizes go through one scan launch whose total comes back
-    with the picked-string bytes in one copy (qh_k_scan_seg): section counts
-    around the 2048-entry tile still give the host writer's bytes."""
+    """Section sizes (16 lanes per section, qh_k_encsec_size) go through one
+    scan launch whose total comes back with the picked-string bytes in one
+    copy (qh_k_scan_seg): section counts around a size wave's, a block's and
+    the scan's 2048-entry tile edges still give the host writer's bytes."""
     src, blocks, plain, strs, lines, line_start = qpack.synth_field_sections(0x5EED0E0 + nsec, nsec)
     dst, secs = enc.encode_sections(plain, strs, lines, line_start)
     assert dst.tobytes() == src.tobytes()
     assert (secs["off"] == blocks["off"]).all() and (secs["len"] == blocks["len"]).all()
+
+
+@pytest.mark.parametrize("bad", ["opcode", "value"])
+def test_encode_sections_rejects_a_bad_line(enc, bad):
+    """One unknown opcode or missing value string anywhere in the batch:
+    QH_ERR_INVALID_ARGUMENT (the size pass's error word), as the host writer
+    rejects it; the batch without it still encodes."""
+    from nghttp3_amd import _lib
+    src, blocks, plain, strs, lines, line_start = qpack.synth_field_sections(0x5EED0BD, 300)
+    lines = lines.copy()
+    with_value = np.flatnonzero(lines["value"] >= 0)
+    k = int(with_value[len(with_value) // 3])
+    if bad == "opcode":
+        lines["opcode"][k] = 99
+    else:
+        lines["value"][k] = -1
+    with pytest.raises(_lib.QhError) as ei:
+        enc.encode_sections(plain, strs, lines, line_start)
+    assert ei.value.code == _lib.QH_ERR_INVALID_ARGUMENT
+    lines0 = qpack.synth_field_sections(0x5EED0BD, 300)[4]
+    dst, _ = enc.encode_sections(plain, strs, lines0, line_start)
+    assert dst.tobytes() == src.tobytes()
 
 
 def test_encode_sections_device_resident(enc):
