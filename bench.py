@@ -712,40 +712,95 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
     return out
 
 
+def _cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max
+    or v1 cfs quota / period), rounded up; None when unlimited / unknown."""
+    import math
+    paths = []
+    try:
+        for line in open("/proc/self/cgroup"):
+            hid, ctl, path = line.rstrip("\n").split(":", 2)
+            if hid == "0":
+                paths.append(("v2", "/sys/fs/cgroup" + path))
+            elif "cpu" in ctl.split(","):
+                paths.append(("v1", "/sys/fs/cgroup/" + ctl + path))
+                paths.append(("v1", "/sys/fs/cgroup/cpu,cpuacct" + path))
+                paths.append(("v1", "/sys/fs/cgroup/cpu" + path))
+    except OSError:
+        pass
+    paths += [("v2", "/sys/fs/cgroup"), ("v1", "/sys/fs/cgroup/cpu"), ("v1", "/sys/fs/cgroup/cpu,cpuacct")]
+    for kind, d in paths:
+        try:
+            if kind == "v2":
+                q, per = open(os.path.join(d, "cpu.max")).read().split()[:2]
+                if q != "max":
+                    return max(1, math.ceil(int(q) / int(per)))
+            else:
+                q = int(open(os.path.join(d, "cpu.cfs_quota_us")).read())
+                per = int(open(os.path.join(d, "cpu.cfs_period_us")).read())
+                if q > 0:
+                    return max(1, math.ceil(q / per))
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def leg_cpu(args, src, spans, total, n):
     """BASELINE.md CPU protocol: the oracle restatement (same nibble FSM and
-    64-bit accumulator as lib/nghttp3_qpack_huffman.c, -O2 -mavx2) round-trips
-    the same strings at T = 1 (a bounded sample) and T = all cores of this
-    process's affinity (the whole batch), each thread on a contiguous shard,
-    CLOCK_MONOTONIC per rep, median of `cpu_reps` reps."""
+    64-bit accumulator as lib/nghttp3_qpack_huffman.c:34-124, -O2 -mavx2)
+    round-trips the same strings at T = 1 (a bounded sample) and T = all
+    CPUs of this process's affinity (the whole batch).  The thread pool is
+    created once, thread t pinned to the t-th CPU of the affinity list and
+    owning a contiguous shard; each encode / decode pass starts and ends at
+    a barrier and repeats the shard until a thread has worked >= 50 ms;
+    verification runs after the timed passes.  min / median / max over
+    `cpu_reps` passes; value = the median round trip."""
     import oracle
     plain = src[:total].cpu().numpy()
     sp = spans.cpu().numpy()
     off = sp[:, 0].astype(np.uint64)
     lens = (sp[:, 1] & 0xFFFFFFFF).astype(np.uint32)
     try:
-        aff = len(os.sched_getaffinity(0))
+        cpus = sorted(os.sched_getaffinity(0))
     except Exception:
-        aff = os.cpu_count() or 1
+        cpus = list(range(os.cpu_count() or 1))
+    # the CPU time this process may use: a cgroup quota (the GPU box grants a
+    # share of its cores) caps the useful thread count below the affinity
+    # list; more threads than that only time-slice and add barrier waits
+    quota = _cpu_quota()
+    nthr = max(1, min(len(cpus), quota)) if quota else len(cpus)
     reps = args.cpu_reps
 
     def run(k, threads):
-        e, d, ok = oracle.bench_roundtrip(plain, off[:k], lens[:k], threads, reps)
+        e, d, ok, inner = oracle.bench_roundtrip(plain, off[:k], lens[:k], threads, reps,
+                                                 cpus=cpus[:threads], min_seconds=0.05)
         b = float(lens[:k].astype(np.uint64).sum())
-        rt = sorted(x + y for x, y in zip(e, d))[len(e) // 2]
-        return {"round_trip_GiBps": round(b / rt / GIB, 4),
-                "decode_GiBps": round(b / sorted(d)[len(d) // 2] / GIB, 4),
-                "encode_GiBps": round(b / sorted(e)[len(e) // 2] / GIB, 4),
+        rt = sorted(b / (x + y) / GIB for x, y in zip(e, d))
+        de = sorted(b / x / GIB for x in d)
+        en = sorted(b / x / GIB for x in e)
+        r4 = lambda v: round(v, 4)
+        return {"round_trip_GiBps": r4(rt[len(rt) // 2]),
+                "round_trip_min_med_max": [r4(rt[0]), r4(rt[len(rt) // 2]), r4(rt[-1])],
+                "decode_GiBps": r4(de[len(de) // 2]),
+                "decode_min_med_max": [r4(de[0]), r4(de[len(de) // 2]), r4(de[-1])],
+                "encode_GiBps": r4(en[len(en) // 2]),
+                "encode_min_med_max": [r4(en[0]), r4(en[len(en) // 2]), r4(en[-1])],
+                "passes_per_rep": list(inner),
                 "strings": int(k), "plain_bytes": int(b), "ok": ok}
 
     k1 = min(n, args.cpu_t1_strings)
     t1 = run(k1, 1)
-    tall = run(n, aff)
-    return {"value": tall["round_trip_GiBps"], "unit": "GiB/s", "cores": aff, "kind": "port",
-            "sample": f"T={aff}: all {n} strings of the rank-0 batch; T=1: the first {k1} "
-                      f"strings; median of {reps} round trips each; oracle/qh_oracle.c "
-                      "-O2 -mavx2 (restatement of lib/nghttp3_qpack_huffman.c)",
-            "t1": t1, "tall": tall, "cpu_model": _cpu_model(),
+    tall = run(n, nthr)
+    return {"value": tall["round_trip_GiBps"], "unit": "GiB/s", "cores": nthr,
+            "kind": "port",
+            "sample": f"T={nthr} pinned threads (affinity {len(cpus)} CPUs, cgroup CPU quota "
+                      f"{quota or 'none'}): all {n} strings of the rank-0 batch; "
+                      f"T=1: the first {k1} strings; {reps} barrier-to-barrier encode and decode "
+                      "passes of >= 50 ms per thread each, verification outside the timed "
+                      "passes, median (min/med/max in t1/tall); oracle/qh_oracle.c -O2 -mavx2 "
+                      "(restatement of lib/nghttp3_qpack_huffman.c)",
+            "t1": t1, "tall": tall, "cpu_model": _cpu_model(), "cpu_quota": quota,
+            "affinity_cpus": len(cpus),
             "equivalence": "restatement-vs-reference speed ratio not measurable: the reference "
                            "needs a generated header absent here (DESIGN.md section 1)"}
 

@@ -41,7 +41,46 @@ def run(lmin, src, spans, total, label, reps=5, decoder="sorted"):
     c.close()
 
 
+def sections(reps=10):
+    """qh_decode_sections_batch (device form, framing sync included) on one
+    field section holding one value of 40,960 encoded bytes (the largest
+    nghttp3 accepts), and on 64 such sections."""
+    import time
+    import numpy as np
+    import torch
+    from nghttp3_amd import qpack, synth
+    text = synth.fill(0x5EED0411, 80000, synth.ALPHABET_A).tobytes()
+    lo, hi = 0, len(text)
+    while lo < hi:  # the longest value whose representation fits the limit
+        mid = (lo + hi + 1) // 2
+        if len(qpack.write_indexed_name(0x50, 5, 4, text[:mid])) <= 1 + 3 + 40960:
+            lo = mid
+        else:
+            hi = mid - 1
+    sec = b"\x00\x00" + qpack.write_indexed_name(0x50, 5, 4, text[:lo])
+    d = qpack.FieldSectionDecoder(0, dtable0=True)
+    for nsec in (1, 64):
+        data = sec * nsec
+        blocks = np.zeros((nsec, 2), dtype=np.int64)
+        blocks[:, 0] = np.arange(nsec) * len(sec)
+        blocks[:, 1] = len(sec)
+        src = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+        blk = torch.from_numpy(blocks).cuda()
+        g = d.decode_blocks_dev(src, blk)
+        torch.cuda.synchronize()
+        ok = bool((g["status"][:nsec] == 0).all()) and int((g["strs"][:1, 1] & 0xFFFFFFFF).item()) == lo
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g = d.decode_blocks_dev(src, blk, g)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) * 1e6 / reps
+        print(json.dumps({"case": f"sections: {nsec} x one value of {len(sec) - 7} encoded B "
+                                  f"({lo} B decoded)", "us": round(us, 1), "ok": ok}), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "sections":
+        return sections()
     import numpy as np
     import torch
     from nghttp3_amd import HuffmanBatchCodec, synth

@@ -251,6 +251,7 @@ struct Record {
   uint64_t stream_id;
   size_t off, len;
   int rv = 0;                     // framing verdict
+  bool partial_bad = false;       // (stream 0) its cut last instruction's Huffman bytes fail
   size_t line0 = 0, nline = 0;    // its lines in `lines`
   size_t span0 = 0, nspan = 0;    // its strings in `spans`
   qh_section_prefix prefix{};
@@ -398,16 +399,69 @@ bool emit(const Table &t, const Record &r, uint64_t ricnt, uint64_t base,
   return true;
 }
 
+// The bytes of an encoder instruction cut by the end of its record.  The
+// reference reads them as they arrive (qpack.c:2815-3150): every Huffman
+// string of the instruction that has begun is decoded over the bytes
+// present (qpack_read_huffman_string, :2737-2763: fin = 1 once the whole
+// string is there), and a failure there fails the record with
+// ENCODER_STREAM_ERROR (:2992-2997, :3083-3088).  True if that happens.
+bool partial_huffman_fails(const uint8_t *p, size_t n) {
+  size_t pos = 0;
+  bool bad = false;
+  // prefixed integer: 1 complete, 0 cut (overflow is the scanner's verdict)
+  auto varint = [&](int prefix, uint64_t &v) -> int {
+    if (pos >= n) return 0;
+    const uint64_t k = (1u << prefix) - 1;
+    v = p[pos++] & k;
+    if (v != k) return 1;
+    for (int shift = 0; pos < n && shift <= 62; shift += 7) {
+      const uint8_t b = p[pos++];
+      v += (uint64_t)(b & 0x7f) << shift;
+      if (!(b & 0x80)) return 1;
+    }
+    return 0;
+  };
+  // one string: 1 complete, 0 cut
+  auto string = [&](int prefix) -> int {
+    if (pos >= n) return 0;
+    const bool h = (p[pos] >> prefix) & 1;
+    uint64_t len = 0;
+    if (varint(prefix, len) != 1) return 0;
+    const size_t have = (size_t)std::min<uint64_t>(len, n - pos);
+    if (h && have) {
+      std::vector<uint8_t> out(nghttp3_qpack_huffman_estimate_decode_length(have) + 1);
+      nghttp3_qpack_huffman_decode_context c;
+      nghttp3_qpack_huffman_decode_context_init(&c);
+      const nghttp3_ssize w = nghttp3_qpack_huffman_decode(&c, out.data(), p + pos, have, have == len);
+      if (w < 0 || nghttp3_qpack_huffman_decode_failure_state(&c)) bad = true;
+    }
+    pos += have;
+    return have == len ? 1 : 0;
+  };
+  if (n == 0) return false;
+  const uint8_t b = p[0];
+  uint64_t idx = 0;
+  if (b & 0x80) {  // insert with name reference: index, value
+    if (varint(6, idx) == 1) string(7);
+  } else if (b & 0x40) {  // insert with literal name: name, value
+    if (string(5) == 1 && !bad) string(7);
+  }
+  return bad;
+}
+
 int decode(const char *outfile, const char *infile) {
   std::vector<uint8_t> file;
   if (!read_file(infile, file)) return -1;
   const size_t n = file.size();
-  // records
+  // records; a framing error ends the list, and is reported after the
+  // records before it were replayed and their output written, as the
+  // reference CLI reads the file record by record (qpack_decode.cc:229-247)
   std::vector<Record> recs;
+  std::string frame_err;
   for (size_t p = 0; p != n;) {
     if (n - p < 12) {
-      std::cerr << "Could not read stream ID and size" << std::endl;
-      return -1;
+      frame_err = "Could not read stream ID and size";
+      break;
     }
     uint64_t sid = 0;
     for (int k = 0; k < 8; ++k) sid = sid << 8 | file[p + k];
@@ -415,9 +469,9 @@ int decode(const char *outfile, const char *infile) {
     for (int k = 0; k < 4; ++k) size = size << 8 | file[p + 8 + k];
     p += 12;
     if (n - p < size) {
-      std::cerr << "Insufficient input: require " << size << " but " << (n - p)
-                << " is available" << std::endl;
-      return -1;
+      frame_err = "Insufficient input: require " + std::to_string(size) + " but " +
+                  std::to_string(n - p) + " is available";
+      break;
     }
     Record r;
     r.stream_id = sid;
@@ -455,6 +509,10 @@ int decode(const char *outfile, const char *infile) {
                                                               tl.data(), tl.size(), &nl, ts.data(),
                                                               ts.size(), &ns);
       if (done >= 0 && (size_t)done < r.len) {
+        // the reference decodes a cut Huffman string's bytes as they arrive
+        // and fails this record if they already fail
+        if (partial_huffman_fails(file.data() + r.off + (size_t)done, r.len - (size_t)done))
+          r.partial_bad = true;
         tail.assign(file.begin() + (std::ptrdiff_t)(r.off + (size_t)done),
                     file.begin() + (std::ptrdiff_t)(r.off + r.len));
         r.len = (size_t)done;
@@ -486,6 +544,7 @@ int decode(const char *outfile, const char *infile) {
             file.data() + r.off, r.len, r.off, lines.data() + nl_tot, lines.size() - nl_tot, &nl,
             spans.data() + ns_tot, spans.size() - ns_tot, &ns);
         r.rv = rv < 0 ? (int)rv : ((size_t)rv != r.len ? QH_ERR_QPACK_ENCODER_STREAM_ERROR : 0);
+        if (r.rv == 0 && r.partial_bad) r.rv = QH_ERR_QPACK_ENCODER_STREAM_ERROR;
       } else {
         r.prefix.reserved = 0xFFFFFFFFu;  // (the parser sets it to 0 once the prefix is read)
         r.rv = qh_qpack_scan_field_section(file.data() + r.off, r.len, r.off, &r.prefix,
@@ -660,6 +719,10 @@ int decode(const char *outfile, const char *infile) {
   }
   double t4 = now_ms();
   of.write(out.data(), (std::streamsize)out.size());
+  if (!frame_err.empty()) {
+    std::cerr << frame_err << std::endl;
+    return -1;
+  }
   if (!blocked.empty()) {
     std::cerr << "Still " << blocked.size() << " stream(s) blocked" << std::endl;
     return -1;

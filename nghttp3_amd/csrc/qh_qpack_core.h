@@ -59,6 +59,10 @@ QH_HD static inline int read_varint(uint64_t *res, const uint8_t **pp, const uin
   return 0;
 }
 
+#ifndef QH_LONG_MIN
+#define QH_LONG_MIN 4096u /* qh_peek_dec.inc kDeferMin */
+#endif
+
 typedef struct scan_out {
   qh_field_line *lines;
   size_t lines_cap, nlines;
@@ -75,6 +79,9 @@ typedef struct scan_out {
   qh_span_in *huff;
   uint64_t *aux;
   uint64_t span_base, huff_base, block;
+  /* Huffman strings of at least QH_LONG_MIN encoded bytes (the GPU
+   * pipeline decodes them a workgroup each, qh_k_dec_long_list) */
+  uint64_t nlong;
 } scan_out;
 
 /* One string literal: H bit at bit `prefix` of the first byte, then the
@@ -132,6 +139,7 @@ QH_HD static inline int read_string(scan_out *o, int32_t *span_idx, const uint8_
   o->nhuff += h ? 1 : 0;
   /* the slot qh_decode_batch gives it: len * 8 / 5 + 16, rounded up to 64 */
   o->hslots += h ? ((len * 8 / 5 + 16 + 63) & ~(uint64_t)63) : 0;
+  o->nlong += h && len >= QH_LONG_MIN ? 1 : 0;
   *pp = p + len;
   return 1;
 }

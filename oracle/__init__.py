@@ -54,9 +54,11 @@ def load():
     lib.qho_encode_batch.restype = ctypes.c_uint64
     lib.qho_decode_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     lib.qho_decode_batch.restype = ctypes.c_uint64
-    lib.qho_bench_roundtrip.argtypes = [vp, vp, vp, sz, ctypes.c_int, ctypes.c_int,
+    lib.qho_bench_roundtrip.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp, ctypes.c_int,
+                                        ctypes.c_double,
                                         ctypes.POINTER(ctypes.c_double),
-                                        ctypes.POINTER(ctypes.c_double)]
+                                        ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int)]
     lib.qho_bench_roundtrip.restype = ctypes.c_int
     _lib = lib
     return lib
@@ -144,12 +146,24 @@ def decode_batch(enc, off, ln):
     return dst, slot[:n], olen[:n], st[:n]
 
 
-def bench_roundtrip(plain, off, ln, nthreads: int, reps: int):
-    """CPU baseline: per-rep (encode seconds, decode seconds) lists and ok."""
+def bench_roundtrip(plain, off, ln, nthreads: int, reps: int, cpus=None,
+                    min_seconds: float = 0.05):
+    """CPU baseline: a pool of `nthreads` threads (thread t pinned to cpus[t]
+    when given), `reps` barrier-to-barrier encode and decode passes, each
+    long enough that a thread works >= min_seconds.  Returns per-rep
+    seconds per round over the strings (encode list, decode list), ok, and
+    the (encode, decode) repetitions per pass."""
     plain = np.ascontiguousarray(plain, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     ln = np.ascontiguousarray(ln, dtype=np.uint32)
     e = (ctypes.c_double * max(reps, 1))()
     d = (ctypes.c_double * max(reps, 1))()
-    rv = load().qho_bench_roundtrip(_p(plain), _p(off), _p(ln), ln.size, nthreads, reps, e, d)
-    return list(e)[:reps], list(d)[:reps], rv == 0
+    inner = (ctypes.c_int * 2)()
+    cp = None
+    if cpus is not None:
+        cpa = np.ascontiguousarray(list(cpus)[:nthreads], dtype=np.int32)
+        assert cpa.size == nthreads
+        cp = _p(cpa)
+    rv = load().qho_bench_roundtrip(_p(plain), _p(off), _p(ln), ln.size, nthreads, cp, reps,
+                                    float(min_seconds), e, d, inner)
+    return list(e)[:reps], list(d)[:reps], rv == 0, (inner[0], inner[1])

@@ -272,7 +272,15 @@ uint64_t qho_decode_batch(const uint8_t *src, const uint64_t *off,
   return nerr;
 }
 
-/* ---- CPU baseline harness ---- */
+/* ---- CPU baseline harness ----
+ *
+ * A pool of T threads is created once, each pinned to its own CPU (the list
+ * the caller passes, else left where the scheduler puts it).  Every timed
+ * pass starts from a barrier and ends at one; a thread runs its contiguous
+ * shard `inner` times per pass, with `inner` calibrated so that a pass takes
+ * at least `min_seconds` per thread (thread wake-up and scheduling noise are
+ * then a small part of the pass).  Verification (decoded bytes == source)
+ * runs after the timed passes, outside them. */
 
 typedef struct {
   const uint8_t *src;
@@ -283,32 +291,66 @@ typedef struct {
   uint64_t *enc_off; /* per string */
   uint8_t *dec;      /* decoded scratch for this shard */
   int ok;
-  int phase; /* 0 = encode, 1 = decode */
+  int cpu;           /* CPU to pin to, -1 = none */
+  uint64_t sink;     /* decoded lengths, so the decode cannot be elided */
+  struct pool *pool;
 } shard_t;
 
-static void *shard_run(void *arg) {
-  shard_t *s = (shard_t *)arg;
+struct pool {
+  pthread_barrier_t start, done;
+  int cmd;   /* 0 encode, 1 decode, 2 verify, -1 exit */
+  int inner;
+};
+
+static void shard_encode(shard_t *s) {
+  uint64_t pos = 0;
   size_t i;
-  if (s->phase == 0) {
-    uint64_t pos = 0;
-    for (i = s->begin; i < s->end; ++i) {
-      size_t h = qho_encode_count(s->src + s->off[i], s->len[i]);
-      s->enc_off[i - s->begin] = pos;
-      qho_encode(s->enc + pos, s->src + s->off[i], s->len[i]);
-      pos += h;
-    }
-    s->enc_off[s->end - s->begin] = pos;
-  } else {
-    for (i = s->begin; i < s->end; ++i) {
-      size_t k = i - s->begin;
-      qho_decode_ctx ctx;
-      qho_decode_context_init(&ctx);
-      uint64_t a = s->enc_off[k], b = s->enc_off[k + 1];
-      ptrdiff_t r = qho_decode(&ctx, s->dec, s->enc + a, (size_t)(b - a), 1);
-      if (r != (ptrdiff_t)s->len[i] ||
-          memcmp(s->dec, s->src + s->off[i], s->len[i]) != 0)
-        s->ok = 0;
-    }
+  for (i = s->begin; i < s->end; ++i) {
+    size_t h = qho_encode_count(s->src + s->off[i], s->len[i]);
+    s->enc_off[i - s->begin] = pos;
+    qho_encode(s->enc + pos, s->src + s->off[i], s->len[i]);
+    pos += h;
+  }
+  s->enc_off[s->end - s->begin] = pos;
+}
+
+static void shard_decode(shard_t *s, int verify) {
+  size_t i;
+  uint64_t sink = 0; /* (a local: shard_t's of adjacent threads share lines) */
+  for (i = s->begin; i < s->end; ++i) {
+    size_t k = i - s->begin;
+    qho_decode_ctx ctx;
+    qho_decode_context_init(&ctx);
+    uint64_t a = s->enc_off[k], b = s->enc_off[k + 1];
+    ptrdiff_t r = qho_decode(&ctx, s->dec, s->enc + a, (size_t)(b - a), 1);
+    sink += (uint64_t)r;
+    if (verify && (r != (ptrdiff_t)s->len[i] ||
+                   memcmp(s->dec, s->src + s->off[i], s->len[i]) != 0))
+      s->ok = 0;
+  }
+  s->sink += sink;
+}
+
+static void *shard_main(void *arg) {
+  shard_t *s = (shard_t *)arg;
+  struct pool *p = s->pool;
+  int it;
+  if (s->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(s->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
+  for (;;) {
+    pthread_barrier_wait(&p->start);
+    if (p->cmd < 0) break;
+    if (p->cmd == 0)
+      for (it = 0; it < p->inner; ++it) shard_encode(s);
+    else if (p->cmd == 1)
+      for (it = 0; it < p->inner; ++it) shard_decode(s, 0);
+    else
+      shard_decode(s, 1);
+    pthread_barrier_wait(&p->done);
   }
   return NULL;
 }
@@ -319,32 +361,43 @@ static double now_s(void) {
   return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-static void run_phase(shard_t *sh, int nthreads, int phase) {
-  pthread_t tid[256];
-  int t;
-  for (t = 0; t < nthreads; ++t) {
-    sh[t].phase = phase;
-    if (nthreads == 1)
-      shard_run(&sh[t]);
-    else
-      pthread_create(&tid[t], NULL, shard_run, &sh[t]);
-  }
-  if (nthreads > 1)
-    for (t = 0; t < nthreads; ++t) pthread_join(tid[t], NULL);
+/* one pass of every thread; seconds from the start barrier to the last
+ * thread's end */
+static double pool_pass(struct pool *p, int cmd, int inner) {
+  p->cmd = cmd;
+  p->inner = inner;
+  double t0 = now_s();
+  pthread_barrier_wait(&p->start);
+  if (cmd >= 0) pthread_barrier_wait(&p->done); /* exit: threads leave */
+  return now_s() - t0;
+}
+
+static int calib_inner(double one, double min_seconds) {
+  double k = one > 0 ? min_seconds / one : 1.0;
+  if (k < 1.0) return 1;
+  if (k > 100000.0) return 100000;
+  return (int)k + 1;
 }
 
 int qho_bench_roundtrip(const uint8_t *src, const uint64_t *off,
-                        const uint32_t *len, size_t n, int nthreads, int reps,
-                        double *enc_seconds, double *dec_seconds) {
-  shard_t sh[256];
-  int t, r, ok = 1;
+                        const uint32_t *len, size_t n, int nthreads,
+                        const int *cpus, int reps, double min_seconds,
+                        double *enc_seconds, double *dec_seconds,
+                        int *inner_out) {
+  shard_t *sh;
+  pthread_t *tid;
+  struct pool p;
+  int t, r, ok = 1, ie, id;
   uint32_t maxlen = 0;
   size_t i;
   init_once();
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 256) nthreads = 256;
+  sh = (shard_t *)calloc((size_t)nthreads, sizeof(shard_t));
+  tid = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   for (i = 0; i < n; ++i)
     if (len[i] > maxlen) maxlen = len[i];
+  pthread_barrier_init(&p.start, NULL, (unsigned)nthreads + 1);
+  pthread_barrier_init(&p.done, NULL, (unsigned)nthreads + 1);
   for (t = 0; t < nthreads; ++t) {
     size_t b = n * (size_t)t / (size_t)nthreads;
     size_t e = n * (size_t)(t + 1) / (size_t)nthreads;
@@ -359,22 +412,34 @@ int qho_bench_roundtrip(const uint8_t *src, const uint64_t *off,
     sh[t].enc_off = (uint64_t *)malloc((e - b + 1) * sizeof(uint64_t));
     sh[t].dec = (uint8_t *)malloc((size_t)maxlen * 30 / 8 * 8 / 5 + 16);
     sh[t].ok = 1;
+    sh[t].cpu = cpus ? cpus[t] : -1;
+    sh[t].pool = &p;
+    pthread_create(&tid[t], NULL, shard_main, &sh[t]);
   }
-  /* one entry per rep (CLOCK_MONOTONIC around each parallel phase) */
+  /* calibration passes (also the warm-up; the encode leaves the encoded
+   * shards the decode passes read) */
+  ie = calib_inner(pool_pass(&p, 0, 1), min_seconds);
+  id = calib_inner(pool_pass(&p, 1, 1), min_seconds);
   for (r = 0; r < reps; ++r) {
-    double t0 = now_s();
-    run_phase(sh, nthreads, 0);
-    double t1 = now_s();
-    run_phase(sh, nthreads, 1);
-    double t2 = now_s();
-    enc_seconds[r] = t1 - t0;
-    dec_seconds[r] = t2 - t1;
+    enc_seconds[r] = pool_pass(&p, 0, ie) / ie;
+    dec_seconds[r] = pool_pass(&p, 1, id) / id;
   }
+  pool_pass(&p, 2, 1); /* verification, untimed */
+  pool_pass(&p, -1, 0);
   for (t = 0; t < nthreads; ++t) {
+    pthread_join(tid[t], NULL);
     ok &= sh[t].ok;
     free(sh[t].enc);
     free(sh[t].enc_off);
     free(sh[t].dec);
+  }
+  pthread_barrier_destroy(&p.start);
+  pthread_barrier_destroy(&p.done);
+  free(sh);
+  free(tid);
+  if (inner_out) {
+    inner_out[0] = ie;
+    inner_out[1] = id;
   }
   return ok ? 0 : -1;
 }

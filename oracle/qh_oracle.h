@@ -70,13 +70,19 @@ uint64_t qho_decode_batch(const uint8_t *src, const uint64_t *off,
                           int32_t *status);
 
 /* CPU baseline: round trip (encode_count + encode, then decode) of the n
- * strings on `nthreads` pthreads, each on a contiguous shard, repeated
- * `reps` times; CLOCK_MONOTONIC seconds of the encode and decode phases of
- * each rep in enc_seconds[r] / dec_seconds[r]. Returns 0 if every string
+ * strings on a pool of `nthreads` threads created once, thread t pinned to
+ * cpus[t] (cpus may be NULL) and owning a contiguous shard.  Each of `reps`
+ * encode and decode passes starts and ends at a barrier and runs the shard
+ * inner[0] (encode) / inner[1] (decode) times, calibrated so that a pass
+ * takes >= min_seconds; enc_seconds[r] / dec_seconds[r] are the pass times
+ * divided by those counts (seconds per round over the n strings).  Decoded
+ * bytes are verified after the timed passes.  Returns 0 if every string
  * round-tripped. */
 int qho_bench_roundtrip(const uint8_t *src, const uint64_t *off,
-                        const uint32_t *len, size_t n, int nthreads, int reps,
-                        double *enc_seconds, double *dec_seconds);
+                        const uint32_t *len, size_t n, int nthreads,
+                        const int *cpus, int reps, double min_seconds,
+                        double *enc_seconds, double *dec_seconds,
+                        int *inner_out);
 
 #ifdef __cplusplus
 }

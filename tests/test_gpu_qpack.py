@@ -85,7 +85,7 @@ def _check_against_oracle(src, blocks, res, refdata, dtable0, strs_dst=None, src
             if want is None:
                 assert int(o["status"]) == -108 and res["verdict"][k] == 0 and res["tokens"][k] == -1
                 continue
-            assert int(o["status"]) == 0
+            assert int(o["status"]) == 0, (b, j, len(want), rspans[j], "binary" if max(want or b"\0") > 126 else "text")
             buf = dst if rspans[j][2] & ref.SPAN_HUFFMAN else src
             got = bytes(buf[int(o["off"]):int(o["off"]) + int(o["len"])])
             assert got == want, (b, j)
@@ -363,3 +363,152 @@ def test_gpu_framing_matches_host_scan_on_netbsd_and_synthetic(dec):
     _same_scan(got, qpack.scan_blocks(src, blocks))
     nl = np.diff(got[2].astype(np.int64))
     assert (nl > 32).sum() > 100 and (nl <= 32).sum() > 100
+
+
+def _max_huffman_text(limit_enc, seed):
+    """Alphabet-A text whose Huffman encoding is exactly limit_enc bytes
+    (or the longest one under it)."""
+    from nghttp3_amd import synth
+    text = synth.fill(seed, limit_enc * 2, synth.ALPHABET_A).tobytes()
+    lo, hi = 0, len(text)
+    while lo < hi:  # longest prefix whose encoding fits
+        mid = (lo + hi + 1) // 2
+        if oracle.encode_count(text[:mid]) <= limit_enc:
+            lo = mid
+        else:
+            hi = mid - 1
+    return text[:lo]
+
+
+def _long_value_sections(seed, nblocks, corrupt=True):
+    """Field sections whose values nghttp3 decodes through the same
+    qpack_read_huffman_string as short ones (qpack.c:2737-2763) up to
+    NGHTTP3_QPACK_MAX_VALUELEN (qpack.h:50; a Huffman value counts as
+    len * 8 / 5, so 40,960 encoded bytes is the largest, read_string
+    qpack.c:3661-3674): Zipf-like lengths of 129 B to 64 KiB, alphabet-A
+    text, binary (all 256 byte values, always Huffman-coded as a foreign
+    encoder may do), and text with 5% binary bytes; values at the limit and
+    one byte past it (-109); literal names; and, when `corrupt`, long strings
+    with EOS inside, zero padding, padding of 8 ones, or the last byte cut."""
+    from nghttp3_amd import synth
+    rng = np.random.default_rng(seed)
+    at_limit = _max_huffman_text(40960, seed)
+    secs, kinds = [], []
+    for b in range(nblocks):
+        sec = bytearray(b"\x00\x00")
+        for f in range(int(rng.integers(1, 4))):
+            kind = int(rng.integers(0, 3))
+            if b % 17 == 3 and f == 0:
+                v = at_limit
+            else:
+                n = int(np.exp(rng.uniform(np.log(129), np.log(65536))))
+                # (under the limit: ~0.82 encoded bytes per text byte, ~0.93
+                # with 5% binary bytes, ~2.9 per binary byte)
+                n = min(n, (48000, 14000, 40000)[kind])
+                v = synth.fill(int(rng.integers(1 << 62)), n, synth.ALPHABET_A).tobytes()
+                if kind == 1:
+                    v = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+                elif kind == 2:
+                    a = np.frombuffer(v, np.uint8).copy()
+                    k = rng.choice(n, max(1, n // 20), replace=False)
+                    a[k] = rng.integers(0, 256, k.size)
+                    v = a.tobytes()
+            enc = bytearray(oracle.encode(v))
+            ck = -1
+            if corrupt and rng.random() < 0.15 and len(enc) > 8:
+                ck = int(rng.integers(0, 4))
+                if ck == 0:    # EOS in the middle
+                    m = len(enc) // 2
+                    enc[m:m + 4] = b"\xff\xff\xff\xff"
+                elif ck == 1:  # zero padding
+                    enc[-1] = 0x00
+                elif ck == 2:  # padding of 8 more ones
+                    enc += b"\xff"
+                else:          # the last code cut
+                    del enc[-1]
+            kinds.append(ck)
+            if rng.random() < 0.25:  # literal name (Huffman), then the value
+                name = synth.fill(int(rng.integers(1 << 62)), int(rng.integers(1, 25)),
+                                  synth.ALPHABET_A).tobytes().lower()
+                ne = oracle.encode(name)
+                sec += ref.put_varint(len(ne), 3, 0x28) + ne
+            else:            # static name reference
+                sec += ref.put_varint(int(rng.integers(0, 99)), 4, 0x50)
+            sec += ref.put_varint(len(enc), 7, 0x80) + bytes(enc)
+        if b % 29 == 5:  # a value one encoded byte past the limit: -109
+            over = oracle.encode(at_limit + b"a" * 8)
+            sec += ref.put_varint(0, 4, 0x50) + ref.put_varint(len(over), 7, 0x80) + over
+        secs.append(bytes(sec))
+    data = b"".join(secs)
+    return np.frombuffer(data, dtype=np.uint8).copy(), _blocks_of([len(x) for x in secs]), kinds
+
+
+def _dev_result(g, nblocks):
+    ns = int(g["nspans"])
+    return {"spans": g["spans"][:ns].cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1),
+            "strs": g["strs"][:ns].cpu().numpy().view(qpack.SPAN_OUT_DTYPE).reshape(-1),
+            "verdict": g["verdict"][:ns].cpu().numpy(), "tokens": g["tokens"][:ns].cpu().numpy(),
+            "span_start": g["span_start"][:nblocks + 1].cpu().numpy().view(np.uint32),
+            "line_start": g["line_start"][:nblocks + 1].cpu().numpy().view(np.uint32),
+            "lines": g["lines"][:int(g["nlines"]) * 24].cpu().numpy().view(qpack.FIELD_LINE_DTYPE),
+            "status": g["status"][:nblocks].cpu().numpy(), "dst": g["dst"].cpu().numpy()}
+
+
+@pytest.mark.parametrize("dtable0", [False, True])
+def test_sections_long_and_binary_values_match_oracle(dec, dec0, refdata, dtable0):
+    """qh_decode_sections_batch on the strings nghttp3 accepts beyond short
+    header text: values of 129 B to the 64 KiB limit (the fused-check
+    decoder hands every string of >= 4 KiB to qh_k_dec_long_list, a
+    workgroup per string), binary and mixed text (long codes on the lanes'
+    careful path), corrupted long strings; host and device forms against
+    oracle/qpack_frame.decode_field_section per block and per string."""
+    import torch
+    d = dec0 if dtable0 else dec
+    src, blocks, kinds = _long_value_sections(0x5EED0410 + dtable0, 240)
+    res = d.decode_blocks(src, blocks)
+    lens = res["spans"]["len"]
+    assert (lens >= 4096).sum() >= 100 and (lens >= 30000).sum() >= 10
+    assert sum(k >= 0 for k in kinds) >= 40
+    nbad = _check_against_oracle(src, blocks, res, refdata, dtable0)
+    assert nbad >= 40
+    assert (res["status"] == qpack.QH_ERR_QPACK_HEADER_TOO_LARGE).sum() >= 5
+    g = d.decode_blocks_dev(torch.from_numpy(src).cuda(),
+                            torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+    torch.cuda.synchronize()
+    gres = _dev_result(g, blocks.size)
+    assert (gres["status"] == res["status"]).all()
+    _check_against_oracle(src, blocks, gres, refdata, dtable0)
+
+
+def test_sections_one_value_at_the_limit(dec0, refdata):
+    """One field section holding one value of 40,960 encoded bytes (the
+    largest nghttp3 accepts), clean and with EOS in its last segment."""
+    v = _max_huffman_text(40960, 0x5EED0411)
+    enc = bytearray(oracle.encode(v))
+    assert len(enc) == 40960
+    for bad in (False, True):
+        e = bytearray(enc)
+        if bad:
+            e[-40:-36] = b"\xff\xff\xff\xff"
+        sec = b"\x00\x00" + ref.put_varint(5, 4, 0x50) + ref.put_varint(len(e), 7, 0x80) + bytes(e)
+        src = np.frombuffer(sec, np.uint8).copy()
+        blocks = _blocks_of([len(sec)])
+        res = dec0.decode_blocks(src, blocks)
+        assert _check_against_oracle(src, blocks, res, refdata, True) == int(bad)
+        if not bad:
+            o = res["strs"][0]
+            assert bytes(res["dst"][int(o["off"]):int(o["off"]) + int(o["len"])]) == v
+
+
+@pytest.mark.parametrize("decoder", ["sorted", "waves"])
+def test_sections_long_values_other_decoders(refdata, decoder):
+    """The same long-value sections through the sorted decoder (its long
+    records, a workgroup each) and the waves decoder."""
+    d = qpack.FieldSectionDecoder(0, dtable0=True)
+    try:
+        d.codec.set_decoder(decoder)
+        src, blocks, _ = _long_value_sections(0x5EED0412, 60)
+        res = d.decode_blocks(src, blocks)
+        _check_against_oracle(src, blocks, res, refdata, True)
+    finally:
+        d.codec.close()

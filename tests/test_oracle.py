@@ -92,3 +92,15 @@ def test_corrupted_corpus_statuses(corpus):
     dst, slot, olen, st = oracle.decode_batch(bad, boff, blen)
     assert (st == corpus["bad_status"]).all()
     assert (olen == corpus["bad_out_len"]).all()
+
+
+def test_cpu_baseline_pool_verifies_and_calibrates(corpus):
+    """The bench's CPU leg: pinned pool, barrier-to-barrier passes, passes
+    repeated until a thread works >= min_seconds, verification untimed."""
+    import os
+    plain, off, ln = corpus["plain"], corpus["off"], corpus["len"]
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    e, d, ok, inner = oracle.bench_roundtrip(plain, off, ln, len(cpus), 3, cpus=cpus,
+                                             min_seconds=0.01)
+    assert ok and len(e) == len(d) == 3
+    assert all(x > 0 for x in e + d) and min(inner) >= 1

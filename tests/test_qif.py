@@ -22,6 +22,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import oracle
 from oracle import qpack_frame as qf
 from oracle import qpack_qif as oq
 from nghttp3_amd import qif, qpack
@@ -251,3 +252,62 @@ def test_driver_scalar_netbsd_summary_matches_reference_cli(tmp_path):
     assert r.returncode == 0, r.stderr
     assert r.stderr.strip().splitlines()[-1] == REFERENCE_NETBSD_S0_LINE
     assert len(out) == 2934 + 12 * 18  # request records: 12-byte header each
+
+
+def _rec(sid, body):
+    return sid.to_bytes(8, "big") + len(body).to_bytes(4, "big") + body
+
+
+# An insert with a literal name "a" whose Huffman value (20 bytes) is cut by
+# the end of its encoder-stream record after 6 bytes; a request (Required
+# Insert Count 0, :method GET) that needs no insert.
+_REQ = b"\x00\x00\xd1"
+
+
+def _cut_insert(bad):
+    value = bytearray(oracle.encode(b"a" * 32))
+    assert len(value) == 20
+    if bad:
+        value[1:5] = b"\xff\xff\xff\xff"  # EOS in the bytes that arrive first
+    head = b"\x41a" + bytes([0x80 | len(value)])
+    return head + bytes(value[:6]), bytes(value[6:])
+
+
+def test_driver_scalar_cut_huffman_string_fails_where_it_arrives(tmp_path):
+    """The reference decodes a cut Huffman string's bytes as they arrive
+    (qpack.c:2737-2763, fin = 0) and fails the encoder-stream record where
+    the EOS code first appears (ENCODER_STREAM_ERROR, :2992-2997, :3083-3088),
+    so the request after that record is never emitted; a cut at the end of
+    the file with bad bytes fails too, a clean one stays pending (exit 0)."""
+    p1, p2 = _cut_insert(True)
+    wire = _rec(0, p1) + _rec(4, _REQ) + _rec(0, p2)
+    r, out = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], wire, "mid")
+    assert r.returncode != 0 and "ENCODER_STREAM_ERROR" in r.stderr, r.stderr
+    assert out == b""
+    r, out = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], _rec(0, p1), "end")
+    assert r.returncode != 0 and "ENCODER_STREAM_ERROR" in r.stderr
+    # the same cut with clean bytes: the request is emitted, the insert
+    # completes in the third record; at the end of the file it stays pending
+    q1, q2 = _cut_insert(False)
+    r, out = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"],
+                  _rec(0, q1) + _rec(4, _REQ) + _rec(0, q2), "clean")
+    assert r.returncode == 0, r.stderr
+    assert out == b":method\tGET\n\n"
+    r, out = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], _rec(0, q1), "pend")
+    assert r.returncode == 0, r.stderr
+
+
+def test_driver_scalar_framing_error_keeps_earlier_output(tmp_path):
+    """A truncated last record: the records before it are decoded and
+    written first, then the framing error ends the run (the reference CLI
+    reads record by record, qpack_decode.cc:229-247)."""
+    data = open(CORPUS, "rb").read()
+    recs = qf.read_qif_out(data)
+    _, off, n = recs[-1]
+    head = data[:off - 12]
+    want = oq.decode_wire(head, 256, 100)
+    assert want.count(b"\n\n") >= 10
+    for cut, msg in ((data[:-3], "Insufficient input"), (head + data[off - 12:off - 5], "Could not read")):
+        r, out = _run(tmp_path, ["--scalar", "-s", "256", "-m", "100", "decode"], cut, "t%d" % len(cut))
+        assert r.returncode != 0 and msg in r.stderr, r.stderr
+        assert out == want
