@@ -40,7 +40,7 @@ def main():
             r = res.cpu().tolist()
             ta = trace.cpu().numpy()
             t = ta[:4 * len(tr)].reshape(-1, 4)
-            tl = ta[4096:].reshape(64, 8)
+            tl = ta[4096:4096 + 512].reshape(64, 8)
             for j in range(64):
                 if tuple(int(x) for x in tl[j]) != lanes0[j]:
                     print("    lane", j, "gpu", tuple(int(x) for x in tl[j]), "model", lanes0[j])
