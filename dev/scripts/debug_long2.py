@@ -46,9 +46,6 @@ def main():
                     print("    lane", j, "gpu", tuple(int(x) for x in tl[j]), "model", lanes0[j])
             got = bytes(d_dst[:r[0]].cpu().numpy())
             first = next((k for k in range(len(tr)) if tuple(int(x) for x in t[k]) != tr[k]), None)
-            tt = ta[8192:8192 + 8 * len(tr)].reshape(-1, 8)[:, :7].astype(np.int64)
-            print("  phase cycles (load+spec, resolve1, wait, resolve2, scan/publish, pack, store), mean over segments:",
-                  [int(x) for x in tt.mean(axis=0)], "first segs:", tt[:3].tolist())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(5):
