@@ -60,10 +60,12 @@ $(ARCHIVE): $(LIBDIR)/qh_device.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(L
 STAMPS := $(LIBDIR)/libqhuff_stamps.so
 stamps: $(STAMPS)
 $(STAMPS): $(CSRC)/qh_device.hip $(CSRC)/*.inc dev/csrc/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
-	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -DQH_STEP_COUNTS=1 -DQH_DEV_VARIANTS -Idev/csrc -c $< -o $(LIBDIR)/qh_device_stamps.o
+	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -DQH_STEP_COUNTS=1 -c $< -o $(LIBDIR)/qh_device_stamps.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_stamps.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
-# Development build with every kernel variant (-DQH_DEV_VARIANTS: decoders
+# Development build with every kernel variant, after
+#   git apply dev/patches/dev_variants_api.patch
+# (the variants' host side, kept out of the product API; -DQH_DEV_VARIANTS: decoders
 # fsm / fsm2 / lut / run / other peek widths and queue shapes, the
 # chunk-engine and streaming encoders), selected by QHUFF_DECODER /
 # QHUFF_ENCODER / QHUFF_CODES; loaded only when QHUFF_LIB points at it
