@@ -93,3 +93,23 @@ abl: $(LIBDIR)/libqhuff_abl$(ABL).so
 $(LIBDIR)/libqhuff_abl$(ABL).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_EW_ABL=$(ABL) -c $< -o $(LIBDIR)/qh_device_abl$(ABL).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_abl$(ABL).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# Framing without the LDS stage (development timing: every block parsed from
+# global memory at the occupancy registers allow) -> libqhuff_frns.so
+frns: $(LIBDIR)/libqhuff_frns.so
+$(LIBDIR)/libqhuff_frns.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_FRAME_NO_STAGE -c $< -o $(LIBDIR)/qh_device_frns.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frns.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# Phase timers without step counts (development: framing phases, dev/scripts/frame_stamps.py)
+frst: $(LIBDIR)/libqhuff_frst.so
+$(LIBDIR)/libqhuff_frst.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_STAMPS -c $< -o $(LIBDIR)/qh_device_frst.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frst.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# The fused encoder at its free register allocation (3 waves per SIMD), for
+# timing against the product's 4 -> libqhuff_ew3.so
+ew3: $(LIBDIR)/libqhuff_ew3.so
+$(LIBDIR)/libqhuff_ew3.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_EW_MIN_WAVES=0 -c $< -o $(LIBDIR)/qh_device_ew3.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_ew3.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

@@ -704,6 +704,21 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
             out[kind]["page_node"] = [_page_node(e_t), _page_node(d_t)]
             # the bound: both directions at once, the probe's time for these bytes
             out[kind]["frac_of_probe_both"] = round(t_both / t_host, 3)
+            # the same batch fanned out over 2 contexts of this GPU
+            # (qh_decode_batch_multi: own streams, host threads, pipelines;
+            # on a node, one context per GPU and link)
+            from nghttp3_amd import HuffmanBatchCodec
+            cs = [HuffmanBatchCodec(dev.index or 0, stream=torch.cuda.Stream(dev)) for _ in range(2)]
+            HuffmanBatchCodec.decode_host_multi(cs, e_h, spn, d_h, o_h)  # warm
+            a = time.perf_counter()
+            for _ in range(reps):
+                HuffmanBatchCodec.decode_host_multi(cs, e_h, spn, d_h, o_h)
+            t_m = (time.perf_counter() - a) / reps
+            out["pinned_2ctx_one_gpu"] = {"decode_GiBps_incl_h2d_d2h": round(total / t_m / GIB, 2),
+                                          "ms": round(t_m * 1e3, 2),
+                                          "frac_of_probe_both": round(t_both / t_m, 3)}
+            for c_ in cs:
+                c_.close()
         del e_t, sp_t, d_t, o_t
     if aff0:
         os.sched_setaffinity(0, aff0)

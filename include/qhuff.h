@@ -231,6 +231,23 @@ QH_EXPORT int qh_decode_batch(qh_ctx *ctx, const uint8_t *src,
                               const qh_span_in *in, size_t n, uint8_t *dst,
                               uint64_t dst_cap, qh_span_out *out, int where);
 
+/* One host-memory batch (as qh_decode_batch with QH_WHERE_HOST) fanned out
+ * over n_ctx contexts -- one per GPU, or several on one GPU with their own
+ * streams: the strings are cut into n_ctx ranges of about equal encoded
+ * bytes, in string order, and context k decodes range k from its own host
+ * thread through its own H2D / decode / D2H pipeline (SURVEY.md section
+ * 8(e): each GPU receives its shard by its own H2D; the reference has no
+ * parallel path).  Range k's decoded strings are packed back to back from
+ * dst + B_k, B_k = the sum of len * 8 / 5 (the reference's
+ * estimate_decode_length, huffman.h:113-115) over the strings of the ranges
+ * before it, so the strings are in global order with a gap between ranges
+ * that never exceeds that estimate's slack; out[i].off is the offset in dst.
+ * dst_cap >= qh_decode_dst_size(in, n) suffices.  Blocks until every range
+ * is done; returns 0 or the first range's error. */
+QH_EXPORT int qh_decode_batch_multi(qh_ctx *const *ctxs, int n_ctx, const uint8_t *src,
+                                    const qh_span_in *in, size_t n, uint8_t *dst,
+                                    uint64_t dst_cap, qh_span_out *out);
+
 /* hlen[i] = nghttp3_qpack_huffman_encode_count(string i). */
 QH_EXPORT int qh_encode_count_batch(qh_ctx *ctx, const uint8_t *src,
                                     const qh_span_in *in, size_t n,

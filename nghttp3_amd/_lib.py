@@ -97,6 +97,7 @@ EXPORTED_FUNCTIONS = (
     "qh_decode_dst_size",
     "qh_encode_dst_bound",
     "qh_decode_batch",
+    "qh_decode_batch_multi",
     "qh_encode_count_batch",
     "qh_encode_batch",
     # QPACK field-line framing (csrc/qh_qpack.c, bound in qpack.py)
@@ -188,6 +189,8 @@ def load():
     lib.qh_encode_dst_bound.restype = u64
     lib.qh_decode_batch.argtypes = [vp, vp, vp, sz, vp, u64, vp, i32]
     lib.qh_decode_batch.restype = i32
+    lib.qh_decode_batch_multi.argtypes = [vp, i32, vp, vp, sz, vp, u64, vp]
+    lib.qh_decode_batch_multi.restype = i32
     lib.qh_encode_count_batch.argtypes = [vp, vp, vp, sz, vp, i32]
     lib.qh_encode_count_batch.restype = i32
     lib.qh_encode_batch.argtypes = [vp, vp, vp, sz, vp, u64, vp, i32]

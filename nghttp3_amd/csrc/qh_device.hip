@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <vector>

@@ -82,6 +82,10 @@ typedef struct scan_out {
   /* Huffman strings of at least QH_LONG_MIN encoded bytes (the GPU
    * pipeline decodes them a workgroup each, qh_k_dec_long_list) */
   uint64_t nlong;
+  /* (the GPU framing's count pass) where each line starts, as an offset
+   * into the section, for its first lstarts_cap lines */
+  uint16_t *lstarts;
+  uint32_t lstarts_cap;
 } scan_out;
 
 /* One string literal: H bit at bit `prefix` of the first byte, then the
@@ -239,6 +243,9 @@ QH_HD static inline int scan_section(scan_out *o, const uint8_t *src, size_t src
     }
     li = o->nlines++; /* (a line cut short by an error is never stored: the
                           callers drop a failed block's lines) */
+    if (o->lstarts && li < o->lstarts_cap) {
+      o->lstarts[li] = (uint16_t)(p - src);
+    }
     cur.index = 0;
     cur.reserved = 0;
     cur.reserved2 = 0;

@@ -288,6 +288,29 @@ class HuffmanBatchCodec:
                    "qh_decode_batch")
         return dst, out
 
+    @staticmethod
+    def decode_host_multi(codecs, src, spans, dst=None, out=None):
+        """qh_decode_batch_multi: one host batch over several contexts (one
+        host thread and H2D / decode / D2H pipeline each); returns (dst,
+        out) with out["off"] global (strings in order, packed per range)."""
+        lib = _lib.load()
+        src = np.ascontiguousarray(src, dtype=np.uint8)
+        spans = np.ascontiguousarray(spans, dtype=SPAN_IN_DTYPE)
+        n = spans.size
+        cap = int(lib.qh_decode_dst_size(spans.ctypes.data_as(ctypes.c_void_p), n))
+        if dst is None:
+            dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        assert dst.dtype == np.uint8 and dst.flags.c_contiguous and dst.size >= cap
+        if out is None:
+            out = np.zeros(n, dtype=SPAN_OUT_DTYPE)
+        ctxs = (ctypes.c_void_p * len(codecs))(*[c._ctx.value for c in codecs])
+        _lib.check(lib.qh_decode_batch_multi(ctxs, len(codecs), src.ctypes.data_as(ctypes.c_void_p),
+                                             spans.ctypes.data_as(ctypes.c_void_p), n,
+                                             dst.ctypes.data_as(ctypes.c_void_p), cap,
+                                             out.ctypes.data_as(ctypes.c_void_p)),
+                   "qh_decode_batch_multi")
+        return dst, out
+
     def encode_count_host(self, src, spans):
         src = np.ascontiguousarray(src, dtype=np.uint8)
         spans = np.ascontiguousarray(spans, dtype=SPAN_IN_DTYPE)

@@ -355,6 +355,53 @@ def test_host_path_full_size_packed_and_pipelined(codec, digests):
     assert end <= half and small[:end].tobytes() == plain[:end].tobytes()
 
 
+@pytest.mark.parametrize("nctx", [2, 4])
+def test_host_path_multi_context(codec, corpus, digests, nctx):
+    """qh_decode_batch_multi: one host batch over nctx contexts on device 0
+    (each with its own stream, host thread and H2D / decode / D2H pipeline;
+    on a node, one context per GPU): config 3 at size, strings in global
+    order, each range packed from its base (the estimate of the ranges before
+    it), every string's bytes the plaintext; the corpus's corrupted strings
+    give the oracle's statuses."""
+    torch = torch_mod()
+    from nghttp3_amd import HuffmanBatchCodec
+    d = digests["c3_A"]
+    src, spans, total = codec.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_A)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    e_h = enc[:d["enc_bytes"]].cpu().numpy()
+    eo = eout.cpu().numpy()
+    sp = np.zeros(d["n"], dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    plain = src[:total].cpu().numpy()
+    lens = ln.cpu().numpy()
+    streams = [torch.cuda.Stream() for _ in range(nctx)]
+    codecs = [HuffmanBatchCodec(0, stream=st) for st in streams]
+    try:
+        dst, out = HuffmanBatchCodec.decode_host_multi(codecs, e_h, sp)
+        assert (out["status"] == 0).all() and (out["len"] == lens).all()
+        assert (np.diff(out["off"].astype(np.int64)) >= out["len"][:-1].astype(np.int64)).all()
+        starts = np.cumsum(lens) - lens
+        gaps = out["off"].astype(np.int64) - starts  # constant within a range
+        assert len(np.unique(gaps)) == nctx and gaps[0] == 0
+        got = np.concatenate([dst[o:o + n_] for o, n_ in
+                              zip(out["off"].astype(np.int64), lens.astype(np.int64))])
+        assert got.tobytes() == plain.tobytes()
+        # corrupted strings: the oracle's statuses, good strings' bytes
+        bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+        bsp = np.zeros(len(blen), dtype=q.SPAN_IN_DTYPE)
+        bsp["off"], bsp["len"] = boff, blen
+        dst2, out2 = HuffmanBatchCodec.decode_host_multi(codecs, bad, bsp)
+        assert (out2["status"] == corpus["bad_status"]).all()
+        assert (out2["len"] == corpus["bad_out_len"]).all()
+    finally:
+        for c in codecs:
+            c.close()
+
+
 def test_host_path_pinned_buffers(codec, corpus, digests):
     """Host-memory decode into pinned dst / out (direct DMA; in development
     builds with QHUFF_HOST_ZC=1 the device-to-host leg as shader stores into
@@ -477,6 +524,50 @@ def _full_size_config(codec, digests, name):
     rep_p = torch.repeat_interleave(poff, ln)
     pos = torch.arange(total, device="cuda", dtype=torch.int64) - rep_p
     assert bool((dec[rep_d + pos] == src[:total]).all())
+
+
+def test_window_decoder_plan_mixed_blocks(codec, corpus):
+    """The window decoder's per-block plan (qh_k_dec_plan): a batch whose
+    first half has 8-256 B lengths (blocks decoded from their windows of
+    consecutive strings) and second half Zipf lengths to 4 KiB with some
+    strings of 4-40 KB (blocks that sort themselves by length class), plus
+    the corpus's corrupted strings spread through both halves: every
+    string's status and bytes are the oracle's, and the output layout is
+    the slot layout (out[i].off = the sum of the slots before string i)."""
+    torch = torch_mod()
+    rng = np.random.default_rng(0x5EED0420)
+    n_half = 1 << 18  # (> 256 strings per block of the 1,024-block cut: the plan sorts only those)
+    ln = np.concatenate([synth.lengths(0x5EED0421, n_half, 8, 256),
+                         synth.zipf_lengths(0x5EED0422, n_half, 1, 4096, 1.2)]).astype(np.uint32)
+    ln[n_half + rng.choice(n_half, 40, replace=False)] = rng.integers(5000, 40000, 40)
+    plain = synth.fill(0x5EED0423, int(ln.sum(dtype=np.uint64)), synth.ALPHABET_A)
+    off = np.concatenate([[0], np.cumsum(ln.astype(np.uint64))[:-1]]).astype(np.uint64)
+    enc, eoff, elen = oracle.encode_batch(plain, off, ln)
+    # corrupted strings in place of some encodings, in both halves
+    bad, boff, blen = corpus["bad"], corpus["bad_off"], corpus["bad_len"]
+    pos = np.sort(rng.choice(2 * n_half, len(blen), replace=False))
+    strs = [enc[int(o):int(o) + int(l)].tobytes() for o, l in zip(eoff, elen)]
+    for k, i in enumerate(pos):
+        strs[i] = bad[int(boff[k]):int(boff[k]) + int(blen[k])].tobytes()
+    src, sp = q.pack_strings(strs)
+    want_dst, want_slot, want_len, want_st = oracle.decode_batch(src, sp["off"], sp["len"])
+    d_src = torch.from_numpy(src.copy()).cuda()
+    d_sp = torch.from_numpy(sp.view(np.int64).reshape(-1, 2).copy()).cuda()
+    cap = int(q.decode_slot_size(sp["len"].astype(np.int64)).sum())
+    d_dst = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros((len(strs), 2), dtype=torch.int64, device="cuda")
+    codec.decode_dev(d_src, d_sp, d_dst, d_out)
+    o, l, st = q.unpack_out(d_out)
+    assert (st == want_st).all() and (l == want_len).all()
+    slots = q.decode_slot_size(sp["len"].astype(np.int64))
+    assert (o == np.concatenate([[0], np.cumsum(slots)[:-1]])).all()
+    dst = d_dst.cpu().numpy()
+    check = np.zeros(len(strs), dtype=bool)
+    check[::7] = True
+    check[pos] = True
+    check[np.nonzero(sp["len"] >= 4096)[0]] = True
+    for i in np.nonzero(check & (st == 0))[0]:
+        assert dst[o[i]:o[i] + l[i]].tobytes() == want_dst[int(want_slot[i]):int(want_slot[i]) + int(l[i])].tobytes(), i
 
 
 @pytest.mark.parametrize("decoder", ["windows", "waves", "sorted"])

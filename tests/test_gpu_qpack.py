@@ -260,8 +260,10 @@ def test_config4_full_corpus_matches_oracle_digests(dec0):
     assert hashlib.sha256(g["tokens"][:ns].cpu().numpy().tobytes()).hexdigest() == d["token_sha256"]
 
 
-def test_check_fields_batch_host_and_device_match_scalar(dec):
+def test_check_fields_batch_host_and_device_match_scalar(dec, refdata):
     import torch
+    from oracle import http_check
+    names, values, _ = refdata
     strs = _check_cases()
     flags = [qpack.SPAN_NAME if i % 2 else 0 for i in range(len(strs))]
     # unaligned, back-to-back packing
@@ -272,6 +274,10 @@ def test_check_fields_batch_host_and_device_match_scalar(dec):
     spans["flags"] = flags
     want = np.array([qpack.check_header_name(x) if f else qpack.check_header_value(x)
                      for x, f in zip(strs, flags)], dtype=np.int8)
+    # the reference's rules (oracle/http_check over the reference's tables)
+    ref_v = np.array([http_check.check_header_name(x, names) if f else
+                      http_check.check_header_value(x, values) for x, f in zip(strs, flags)], dtype=np.int8)
+    assert (want == ref_v).all()
     got = qpack.check_fields_host(dec.codec, src, spans)
     assert (got == want).all()
     # device-resident, padded buffer
@@ -287,13 +293,16 @@ def test_check_fields_batch_host_and_device_match_scalar(dec):
 def test_lookup_tokens_batch_host_and_device_match_scalar(dec):
     import torch
     from conftest import load_json
+    from oracle import http_check
     from test_http_check import token_cases
-    names = token_cases(load_json("tokens.json")["tokens"], 0x5EED0F8)
+    tokens = load_json("tokens.json")["tokens"]
+    names = token_cases(tokens, 0x5EED0F8)
     src = np.frombuffer(b"\x00" * 5 + b"".join(names), dtype=np.uint8)
     spans = np.zeros(len(names), dtype=SPAN_IN_DTYPE)
     spans["len"] = [len(x) for x in names]
     spans["off"] = 5 + np.concatenate([[0], np.cumsum(spans["len"].astype(np.uint64))[:-1]])
     want = np.array([qpack.lookup_token(x) for x in names], dtype=np.int32)
+    assert (want == np.array([http_check.lookup_token(x, tokens) for x in names])).all()
     assert (want >= 0).sum() >= 61  # every token name, plus random hits
     assert (qpack.lookup_tokens_host(dec.codec, src, spans) == want).all()
     d_src = torch.from_numpy(src.copy()).cuda()
