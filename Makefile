@@ -101,6 +101,13 @@ $(LIBDIR)/libqhuff_frns.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_commo
 	$(HIPCC) $(HIPFLAGS) -DQH_FRAME_NO_STAGE -c $< -o $(LIBDIR)/qh_device_frns.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frns.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
+# Count-pass ablations (development timing: make frx FRX=<mask>, see
+# QH_FR_ABL in qh_frame.inc) -> libqhuff_frx<mask>.so
+frx: $(LIBDIR)/libqhuff_frx$(FRX).so
+$(LIBDIR)/libqhuff_frx$(FRX).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_FR_ABL=$(FRX) -c $< -o $(LIBDIR)/qh_device_frx$(FRX).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frx$(FRX).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
 # Phase timers without step counts (development: framing phases, dev/scripts/frame_stamps.py)
 frst: $(LIBDIR)/libqhuff_frst.so
 $(LIBDIR)/libqhuff_frst.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

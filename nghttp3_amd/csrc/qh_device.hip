@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <atomic>
 #include <thread>
 #include <string>
 #include <type_traits>
