@@ -105,6 +105,30 @@ def test_encode_sections_device_resident(enc):
         enc.encode_sections_dev(t_plain, t_strs, t_lines, t_ls, small, t_sec)
 
 
+def test_encode_sections_device_resident_growing_batches():
+    """The device form queues the picked strings' codes before it reads the
+    totals, into scratch sized by earlier calls, and sizes its per-line
+    offsets by the most lines seen so far: a fresh context fed batches that
+    grow and shrink (each growth re-runs the size pass and the codes after
+    the sync) writes the host writer's bytes every time."""
+    import torch
+    enc = qpack.FieldSectionEncoder(0)
+    for nsec in (3, 2049, 10, 4097, 64):
+        src, blocks, plain, strs, lines, line_start = qpack.synth_field_sections(0x5EED0C6 + nsec, nsec)
+        t_plain = torch.from_numpy(plain.copy()).cuda()
+        t_strs = torch.from_numpy(strs.view(np.int64).reshape(-1, 2).copy()).cuda()
+        t_lines = torch.from_numpy(lines.view(np.uint8).copy()).cuda()
+        t_ls = torch.from_numpy(line_start.view(np.int32).copy()).cuda()
+        t_dst = torch.zeros(src.size + 64, dtype=torch.uint8, device="cuda")
+        t_sec = torch.zeros((nsec, 2), dtype=torch.int64, device="cuda")
+        need = enc.encode_sections_dev(t_plain, t_strs, t_lines, t_ls, t_dst, t_sec)
+        torch.cuda.synchronize()
+        assert need == src.size, nsec
+        assert t_dst[:need].cpu().numpy().tobytes() == src.tobytes(), nsec
+        sec = t_sec.cpu().numpy()
+        assert (sec[:, 0] == blocks["off"].astype(np.int64)).all(), nsec
+
+
 def test_c_program_decodes_and_reencodes_corpus_sections(tmp_path):
     exe = tmp_path / "sections_roundtrip"
     libdir = os.path.join(ROOT, "nghttp3_amd", "lib")

@@ -208,6 +208,29 @@ def test_sections_pipeline_at_scan_tile_edges(dec0, refdata, nblocks):
     assert lines.tobytes() == res["lines"].tobytes()
 
 
+def test_sections_device_growing_batches(refdata):
+    """The device form queues its write pass before it reads framing's
+    totals, into scratch laid out for the most spans seen so far: a fresh
+    context fed batches that grow (the write runs again after the sync) and
+    shrink gives the oracle's results every time."""
+    import torch
+    d = qpack.FieldSectionDecoder(0, dtable0=True)
+    for nblocks in (3, 2049, 10, 4097, 700):
+        src, blocks, _ = _corrupted_corpus(0x5EED00F0 + nblocks, nblocks)
+        g = d.decode_blocks_dev(torch.from_numpy(src).cuda(),
+                                torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda())
+        torch.cuda.synchronize()
+        ns = int(g["nspans"])
+        gres = {"spans": g["spans"][:ns].cpu().numpy().view(SPAN_IN_DTYPE).reshape(-1),
+                "strs": g["strs"][:ns].cpu().numpy().view(qpack.SPAN_OUT_DTYPE).reshape(-1),
+                "verdict": g["verdict"][:ns].cpu().numpy(), "tokens": g["tokens"][:ns].cpu().numpy(),
+                "span_start": g["span_start"][:nblocks + 1].cpu().numpy().view(np.uint32),
+                "line_start": g["line_start"][:nblocks + 1].cpu().numpy().view(np.uint32),
+                "lines": g["lines"][:int(g["nlines"]) * 24].cpu().numpy().view(qpack.FIELD_LINE_DTYPE),
+                "status": g["status"][:nblocks].cpu().numpy(), "dst": g["dst"].cpu().numpy()}
+        _check_against_oracle(src, blocks, gres, refdata, True)
+
+
 def test_sections_pipeline_clean_blocks_give_the_writer_plaintext(dec0):
     src, blocks, plain, strs, lines, ls = qpack.synth_field_sections(0x5EED000A, 3000)
     res = dec0.decode_blocks(src, blocks)
