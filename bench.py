@@ -346,6 +346,7 @@ def main():
         dec5.zero_()
         codec.decode_dev(enc5, eout5, dec5, dout5)
         ok5 = roundtrip_ok(src5, sp5, dec5, dout5) and ok5_alt
+        codec.set_encoder("windows")
         te5_alt = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 3)
         enc5_alt, eout5_alt = enc5[:eb5].clone(), eout5.clone()
         codec.set_encoder("fused")
@@ -355,12 +356,19 @@ def main():
         del enc5_alt, eout5_alt
         te5 = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 5)
         td5 = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 5)
+        # the library defaults on the same batch (QH_ENCODER_AUTO, the
+        # window decoder with its per-block plan)
+        codec.set_encoder("auto")
+        codec.set_decoder("windows")
+        te5_def = timed(lambda: codec.encode_dev(src5, sp5, enc5, eout5), 3)
+        td5_def = timed(lambda: codec.decode_dev(enc5, eout5, dec5, dout5), 3)
+        codec.set_decoder("sorted")
         codec.enable_timing(True)
         for _ in range(3):
             codec.decode_dev(enc5, eout5, dec5, dout5)
         k5 = kernel_table(codec.kernel_times(), sp5.shape[0], tot5, eb5)
         codec.enable_timing(False)
-        codec.set_encoder("windows")
+        codec.set_encoder("auto")
         codec.set_decoder("windows")
         d5 = k5.get("qh_k_dec_peek", {})
         p5, e5 = D.sum(float(tot5)), D.sum(float(eb5))
@@ -374,6 +382,8 @@ def main():
                    "decode_GiBps_wave_decoder": round(p5 / D.max(td5_alt) / GIB, 2),
                    "encoder": "fused (qh_k_encw: lengths and codes in one pass over the plaintext)",
                    "encode_GiBps_window_encoder": round(p5 / D.max(te5_alt) / GIB, 2),
+                   "encode_GiBps_default_auto": round(p5 / D.max(te5_def) / GIB, 2),
+                   "decode_GiBps_default_windows_plan": round(p5 / D.max(td5_def) / GIB, 2),
                    "decode_kernels_us_rank0": {k: v["avg_us"] for k, v in k5.items()},
                    "round_trip_GiBps": round(p5 / (te5 + td5) / GIB, 2),
                    "decode_kernel_us_rank0": d5.get("avg_us"),
@@ -397,7 +407,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_configs:
         u_src, u_spans, u_total = codec.synth(args.seed, args.strings, args.min_len, args.max_len, synth.ALPHABET_U)
         u_enc, u_eout, u_eb, u_dec, u_dout = buffers(u_src, u_spans)
+        codec.set_encoder("windows")
         tue_win = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 3)
+        codec.set_encoder("auto")
+        tue_def = timed(lambda: codec.encode_dev(u_src, u_spans, u_enc, u_eout), 3)
         codec.set_encoder("fused")  # (binary text: the one-pass encoder, the sorted decoder)
         codec.set_decoder("sorted")
         u_enc.zero_()
@@ -408,12 +421,14 @@ def main():
         tud = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 5)
         codec.set_decoder("windows")
         tud_win = timed(lambda: codec.decode_dev(u_enc, u_eout, u_dec, u_dout), 3)
-        codec.set_encoder("windows")
+        codec.set_encoder("auto")
         configU = {"strings": args.strings, "plain_bytes": u_total, "enc_bytes": u_eb,
                    "encode_GiBps": round(u_total / tue / GIB, 2), "encoder": "fused",
                    "encode_GiBps_window_encoder": round(u_total / tue_win / GIB, 2),
+                   "encode_GiBps_default_auto": round(u_total / tue_def / GIB, 2),
                    "decode_GiBps": round(u_total / tud / GIB, 2), "decoder": "sorted",
                    "decode_GiBps_window_decoder": round(u_total / tud_win / GIB, 2),
+                   "decode_GiBps_default_windows_plan": round(u_total / tud_win / GIB, 2),
                    "round_trip_GiBps": round(u_total / (tue + tud) / GIB, 2), "bit_exact": u_ok}
         del u_src, u_spans, u_enc, u_eout, u_dec, u_dout
 

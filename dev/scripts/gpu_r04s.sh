@@ -1,6 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04x; mkdir -p $O
+O=gpurun_out/r04y; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; grep -E "FAILED|^E " $O/pytest.log | head -20
 [ $rc -ne 0 ] && exit $rc

@@ -186,7 +186,11 @@ QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
 #define QH_DECODER_SORTED 2
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 /* Codes kernel of qh_encode_batch (results are identical; speed is not):
- * QH_ENCODER_WINDOWS (default) encodes a sorted window of up to 256 strings
+ * QH_ENCODER_AUTO (default) picks one of the two below per batch on the
+ * device, from a sample of 16,384 strings (their lengths' spread and mean,
+ * their first bytes): QH_ENCODER_FUSED for skewed, long or binary strings,
+ * else QH_ENCODER_WINDOWS.
+ * QH_ENCODER_WINDOWS encodes a sorted window of up to 256 strings
  * per workgroup into an LDS stage copied out with coalesced stores --
  * fastest for strings of similar length; QH_ENCODER_WAVES lets every wave
  * sort and encode its own chunks of 256 strings with no workgroup barrier,
@@ -199,6 +203,7 @@ QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
  * string, a decoupled look-back over 4 KiB tiles places each tile in the dense
  * output, and the codes go out through an LDS stage. */
 #define QH_ENCODER_FUSED 2
+#define QH_ENCODER_AUTO 3
 QH_EXPORT int qh_ctx_set_encoder(qh_ctx *ctx, int kind);
 QH_EXPORT void *qh_ctx_stream(qh_ctx *ctx);
 /* Wait for all work queued on the context's stream. */

@@ -30,6 +30,7 @@ QH_DECODER_SORTED = 2
 QH_ENCODER_WINDOWS = 0
 QH_ENCODER_WAVES = 1
 QH_ENCODER_FUSED = 2
+QH_ENCODER_AUTO = 3
 
 NGHTTP3_QPACK_HUFFMAN_FLAG_ACCEPTED = 0x01
 NGHTTP3_QPACK_HUFFMAN_FLAG_SYM = 0x02

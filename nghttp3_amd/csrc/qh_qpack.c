@@ -35,7 +35,7 @@ QH_EXPORT int qh_qpack_scan_field_section(
   const uint8_t *src, size_t srclen, uint64_t src_off,
   qh_section_prefix *prefix, qh_field_line *lines, size_t lines_cap,
   size_t *nlines, qh_span_in *spans, size_t spans_cap, size_t *nspans) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
+  scan_out o = {.lines = lines, .lines_cap = lines_cap, .spans = spans, .spans_cap = spans_cap};
   int rv;
 
   if ((src == NULL && srclen) || nlines == NULL || nspans == NULL ||
@@ -54,7 +54,7 @@ QH_EXPORT int qh_qpack_scan_blocks(const uint8_t *src,
                                    qh_span_in *spans, size_t spans_cap,
                                    uint32_t *line_start, uint32_t *span_start,
                                    int32_t *status) {
-  scan_out o = {lines, lines_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
+  scan_out o = {.lines = lines, .lines_cap = lines_cap, .spans = spans, .spans_cap = spans_cap};
   size_t i;
 
   if ((src == NULL && nblocks) || (blocks == NULL && nblocks) ||
@@ -90,7 +90,7 @@ QH_EXPORT nghttp3_ssize qh_qpack_scan_encoder_stream(
   const uint8_t *src, size_t srclen, uint64_t src_off, qh_field_line *insts,
   size_t insts_cap, size_t *ninsts, qh_span_in *spans, size_t spans_cap,
   size_t *nspans) {
-  scan_out o = {insts, insts_cap, 0, spans, spans_cap, 0, {0, 0, 0, 0, 0, 0, 0}, 0, 0, 0};
+  scan_out o = {.lines = insts, .lines_cap = insts_cap, .spans = spans, .spans_cap = spans_cap};
   const uint8_t *p = src, *end = src + srclen, *done = src;
   const int bad = QH_ERR_QPACK_ENCODER_STREAM_ERROR;
   const int big = QH_ERR_QPACK_HEADER_TOO_LARGE; /* qpack.c:2962-2972 */

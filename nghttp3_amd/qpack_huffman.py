@@ -176,10 +176,11 @@ class HuffmanBatchCodec:
         _lib.check(self._lib.qh_ctx_set_decoder(self._ctx, k), "qh_ctx_set_decoder")
 
     def set_encoder(self, kind: str):
-        """'windows' (default: strings of similar length), 'waves' or 'fused'
-        (one pass: long strings, binary text); results are identical."""
+        """'auto' (default: chosen per batch on the device), 'windows'
+        (strings of similar length), 'waves' or 'fused' (one pass: long,
+        skewed or binary strings); results are identical."""
         k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES,
-             "fused": _lib.QH_ENCODER_FUSED}[kind]
+             "fused": _lib.QH_ENCODER_FUSED, "auto": _lib.QH_ENCODER_AUTO}[kind]
         _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")
 
     def sync(self):
