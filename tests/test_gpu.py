@@ -1019,11 +1019,14 @@ def test_zipf_lengths_roundtrip(codec, alphabet):
         assert dst[do[j]:do[j] + dl[j]].tobytes() == plain[off[j]:off[j] + ln[j]].tobytes(), j
 
 
-# The two shipped encoders (qh_ctx_set_encoder): the window encoder (a
-# sorted 256-string window per workgroup, LDS stage, coalesced copy-out) and
-# the wave encoder (per-wave sorted chunks, LDS rings, per-lane 16-byte
-# output chunks).
-ENCODERS = ["windows", "waves", "fused"]
+# The shipped encoders (qh_ctx_set_encoder): the window encoder (a sorted
+# 256-string window per workgroup, LDS stage, coalesced copy-out), the wave
+# encoder (per-wave sorted chunks, LDS rings, per-lane 16-byte output
+# chunks), the fused one-pass encoder, and the default that picks one of
+# the window and fused encoders per batch on the device (QH_ENCODER_AUTO:
+# the text cases here take the window path, Zipf, mixed and binary the
+# fused one).
+ENCODERS = ["windows", "waves", "fused", "auto"]
 
 
 @pytest.mark.parametrize("kind", ENCODERS)
