@@ -24,7 +24,7 @@ $(LIBDIR)/qh_scalar.o: $(CSRC)/qh_scalar.c $(CSRC)/qh_tables.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(CSRC)/qh_tables.h $(CSRC)/qh_tokens.h $(CSRC)/qh_qpack_core.h include/qhuff.h
+$(LIBDIR)/qh_device.o: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(CSRC)/qh_tables.h $(CSRC)/qh_tokens.h $(CSRC)/qh_qpack_core.h $(CSRC)/qh_frame_fast.h include/qhuff.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
