@@ -1,6 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04ad; mkdir -p $O
+O=gpurun_out/r04ae; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; grep -E "FAILED|^E " $O/pytest.log | head -20
 [ $rc -ne 0 ] && exit $rc

@@ -186,9 +186,10 @@ QH_EXPORT int qh_ctx_set_stream(qh_ctx *ctx, void *stream);
 #define QH_DECODER_SORTED 2
 QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 /* Codes kernel of qh_encode_batch (results are identical; speed is not):
- * QH_ENCODER_AUTO (default) picks one of the two below per batch on the
- * device, from a sample of 16,384 strings (their lengths' spread and mean,
- * their first bytes): QH_ENCODER_FUSED for skewed, long or binary strings,
+ * QH_ENCODER_AUTO (default) runs one of the two below per batch, chosen
+ * from the strings of the context's previous encode (their lengths' spread
+ * and mean, their encoded size; the first encode of a context uses the
+ * window encoder): QH_ENCODER_FUSED for skewed, long or binary strings,
  * else QH_ENCODER_WINDOWS.
  * QH_ENCODER_WINDOWS encodes a sorted window of up to 256 strings
  * per workgroup into an LDS stage copied out with coalesced stores --
