@@ -108,6 +108,13 @@ $(LIBDIR)/libqhuff_frx$(FRX).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_
 	$(HIPCC) $(HIPFLAGS) -DQH_FR_ABL=$(FRX) -c $< -o $(LIBDIR)/qh_device_frx$(FRX).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frx$(FRX).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
+# Length-pass ablations (development timing: make lx LX=<mask>, see
+# QH_LX_ABL in qh_lane_enc.inc) -> libqhuff_lx<mask>.so
+lx: $(LIBDIR)/libqhuff_lx$(LX).so
+$(LIBDIR)/libqhuff_lx$(LX).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_LX_ABL=$(LX) -c $< -o $(LIBDIR)/qh_device_lx$(LX).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_lx$(LX).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
 # Phase timers without step counts (development: framing phases, dev/scripts/frame_stamps.py)
 frst: $(LIBDIR)/libqhuff_frst.so
 $(LIBDIR)/libqhuff_frst.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

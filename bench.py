@@ -283,7 +283,6 @@ def main():
             "qh_k_dec_peek": encb + plain + 32 * n,          # E + D + 16 B span in + 16 B out
             "qh_k_dec_reserve": 16 * n,                      # spans in
             "qh_k_enc_lens_stream": plain + 16 * n + 8 * n,  # D + spans in + len/status out
-            "qh_k_enc_lens_lane": plain + 16 * n + 8 * n,
             "qh_k_enc_lanes": plain + encb + 16 * n + 8 * n + 16 * n,  # D + E + spans
             "qh_k_encw": plain + encb + 16 * n + 16 * n,     # D + E + spans in + out
             "qh_k_sched_count": 16 * n,                      # spans in

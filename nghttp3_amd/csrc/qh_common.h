@@ -164,6 +164,61 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Wave-wide reductions with DPP row shifts and row broadcasts (no LDS round
+// trips: a __shfl_xor step is a ds_bpermute and a wait on it).  Every lane of
+// the wave must be active; the result is lane 63's, read into every lane.
+// A lane whose DPP source lies outside its row keeps `ident` (bound_ctrl off).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v, uint32_t ident) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v, uint64_t ident) {
+  return (uint64_t)dpp_u32<CTRL, ROWS>((uint32_t)v, (uint32_t)ident) |
+         (uint64_t)dpp_u32<CTRL, ROWS>((uint32_t)(v >> 32), (uint32_t)(ident >> 32)) << 32;
+}
+__device__ __forceinline__ uint32_t lane63_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint64_t lane63_u64(uint64_t v) {
+  return (uint64_t)lane63_u32((uint32_t)v) | (uint64_t)lane63_u32((uint32_t)(v >> 32)) << 32;
+}
+// Inclusive scan (lane i: op over lanes 0..i); T is uint32_t or uint64_t.
+template <typename T, typename F>
+__device__ __forceinline__ T wave_incl_dpp(T v, T ident, F op) {
+  if constexpr (sizeof(T) == 4) {
+    v = op(v, dpp_u32<0x111, 0xf>(v, ident));  // row_shr:1
+    v = op(v, dpp_u32<0x112, 0xf>(v, ident));  // row_shr:2
+    v = op(v, dpp_u32<0x114, 0xf>(v, ident));  // row_shr:4
+    v = op(v, dpp_u32<0x118, 0xf>(v, ident));  // row_shr:8
+    v = op(v, dpp_u32<0x142, 0xa>(v, ident));  // row_bcast:15
+    v = op(v, dpp_u32<0x143, 0xc>(v, ident));  // row_bcast:31
+  } else {
+    v = op(v, dpp_u64<0x111, 0xf>(v, ident));
+    v = op(v, dpp_u64<0x112, 0xf>(v, ident));
+    v = op(v, dpp_u64<0x114, 0xf>(v, ident));
+    v = op(v, dpp_u64<0x118, 0xf>(v, ident));
+    v = op(v, dpp_u64<0x142, 0xa>(v, ident));
+    v = op(v, dpp_u64<0x143, 0xc>(v, ident));
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t v) {
+  return wave_incl_dpp<uint32_t>(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint64_t wave_scan_add_u64(uint64_t v) {
+  return wave_incl_dpp<uint64_t>(v, 0ull, [](uint64_t a, uint64_t b) { return a + b; });
+}
+__device__ __forceinline__ uint64_t wave_add_u64(uint64_t v) {
+  return lane63_u64(wave_incl_dpp<uint64_t>(v, 0ull, [](uint64_t a, uint64_t b) { return a + b; }));
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  return lane63_u64(wave_incl_dpp<uint64_t>(v, ~0ull, [](uint64_t a, uint64_t b) { return a < b ? a : b; }));
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  return lane63_u64(wave_incl_dpp<uint64_t>(v, 0ull, [](uint64_t a, uint64_t b) { return a > b ? a : b; }));
+}
+
 // Block-level sum of per-thread counters -> one atomic per block.
 __device__ __forceinline__ void block_add(unsigned long long *dst,
                                           unsigned long long v,
