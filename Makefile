@@ -115,6 +115,13 @@ $(LIBDIR)/libqhuff_lx$(LX).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_co
 	$(HIPCC) $(HIPFLAGS) -DQH_LX_ABL=$(LX) -c $< -o $(LIBDIR)/qh_device_lx$(LX).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_lx$(LX).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
+# Codes-pass ablations (development timing: make la LA=<mask>, see QH_LA_ABL
+# in qh_lane_enc.inc) -> libqhuff_la<mask>.so
+la: $(LIBDIR)/libqhuff_la$(LA).so
+$(LIBDIR)/libqhuff_la$(LA).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_LA_ABL=$(LA) -c $< -o $(LIBDIR)/qh_device_la$(LA).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_la$(LA).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
 # Phase timers without step counts (development: framing phases, dev/scripts/frame_stamps.py)
 frst: $(LIBDIR)/libqhuff_frst.so
 $(LIBDIR)/libqhuff_frst.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
