@@ -22,8 +22,7 @@ LAYOUT = {
                   4: "iter body", 5: "careful", 6: "str end"}, 11, 10, None),
     "enc_lens": ({0: "head", 2: "dma wait", 3: "lookups", 4: "scan", 5: "ends", 6: "tail"},
                  10, 10, 11),
-    "enc_lanes": ({0: "head", 1: "wait+zero", 2: "bits+scan", 3: "starts", 4: "emit",
-                   5: "copy"}, 10, 10, 11),
+    "enc_lanes": ({0: "setup", 1: "encode", 2: "copy-out"}, 10, 10, None),
 }
 
 
