@@ -212,6 +212,12 @@ __device__ __forceinline__ uint64_t wave_scan_add_u64(uint64_t v) {
 __device__ __forceinline__ uint64_t wave_add_u64(uint64_t v) {
   return lane63_u64(wave_incl_dpp<uint64_t>(v, 0ull, [](uint64_t a, uint64_t b) { return a + b; }));
 }
+__device__ __forceinline__ uint32_t wave_add_u32(uint32_t v) {
+  return lane63_u32(wave_scan_add_u32(v));
+}
+__device__ __forceinline__ uint32_t wave_max_u32_all(uint32_t v) {
+  return lane63_u32(wave_incl_dpp<uint32_t>(v, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; }));
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return lane63_u64(wave_incl_dpp<uint64_t>(v, ~0ull, [](uint64_t a, uint64_t b) { return a < b ? a : b; }));
 }
