@@ -952,8 +952,9 @@ def test_long_strings_wave_per_string(alphabet, decoder):
 @pytest.mark.parametrize("mode", ["default", "lane"])
 def test_encode_length_passes(mode, corpus, digests):
     """The encoder's passes: streaming lengths + lane-per-string codes
-    (default), and every window's lengths left to the lane-per-string pass
-    (QHUFF_DEBUG=4) -- corpus lengths/codes, counts, overlapping and scattered spans, and the
+    (default), and every window's lengths counted a lane per string inside
+    the length kernel (QHUFF_DEBUG=4, the scattered-window path) -- corpus
+    lengths/codes, counts, overlapping and scattered spans, and the
     full-size c2_U digest."""
     import os
     from nghttp3_amd import HuffmanBatchCodec
@@ -982,7 +983,7 @@ def test_encode_length_passes(mode, corpus, digests):
         enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8,
                           device="cuda")
         eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
-        for _ in range(2):  # the second call reuses the other window-list counter
+        for _ in range(2):  # (the second call: the double-buffered stats and totals)
             c.encode_dev(src, spans, enc, eout)
             st = c.stats()
             assert st["n_errors"] == 0 and st["out_bytes"] == d["enc_bytes"]
