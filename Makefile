@@ -122,6 +122,13 @@ $(LIBDIR)/libqhuff_la$(LA).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_co
 	$(HIPCC) $(HIPFLAGS) -DQH_LA_ABL=$(LA) -c $< -o $(LIBDIR)/qh_device_la$(LA).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_la$(LA).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 
+# Dense-pack ablations (development timing: make dp DP=<mask>, see QH_DP_ABL
+# in qh_host.inc) -> libqhuff_dp<mask>.so
+dp: $(LIBDIR)/libqhuff_dp$(DP).so
+$(LIBDIR)/libqhuff_dp$(DP).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_DP_ABL=$(DP) -c $< -o $(LIBDIR)/qh_device_dp$(DP).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_dp$(DP).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
 # Phase timers without step counts (development: framing phases, dev/scripts/frame_stamps.py)
 frst: $(LIBDIR)/libqhuff_frst.so
 $(LIBDIR)/libqhuff_frst.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
