@@ -16,7 +16,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("QHUFF_LIB", os.path.join(ROOT, "nghttp3_amd", "lib", "libqhuff_dev.so"))
+_DEV = os.path.join(ROOT, "nghttp3_amd", "lib", "libqhuff_dev.so")
+if os.path.exists(_DEV):  # (else the product library: its kPeekVariants entries)
+    os.environ.setdefault("QHUFF_LIB", _DEV)
 
 
 def main():

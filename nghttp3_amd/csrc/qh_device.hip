@@ -54,6 +54,7 @@
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #endif
 #include "qh_peek_dec.inc"   // decoders (windows: default; waves): W-bit peek table + leading-ones table
+#include "qh_pair_dec.inc"   // decoder: two codes per lookup, waves fed from a group queue
 #ifdef QH_DEV_VARIANTS
 #include "qh_dec3.inc"       // decoder: plan + task-queue lanes
 #endif
