@@ -433,8 +433,11 @@ def main():
 
     # ---- PCIe-inclusive host path (reported, never the value) ----
     host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path:
+    if world == 1 and not args.no_host_path:
         host_path = leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev)
+    elif not args.no_host_path:
+        # every rank its shard from host memory, over its own link
+        host_path = leg_host_path_ranks(torch, codec, q, src, enc, eout, enc_bytes, total, n, dev, D, rank, world)
 
     # ---- CPU baseline (rank 0, N = 1) ----
     cpu = None
@@ -488,8 +491,8 @@ def leg_config4(args, torch, dev, codec, D, rank, world, timed):
     from nghttp3_amd import qpack as qp
     from nghttp3_amd import shard
     nb_all = args.c4_blocks
-    lo, hi = shard.block_range(rank, world, nb_all)
     q_src, q_blocks, q_plain, q_strs, q_lines, q_ls = qp.synth_field_sections(SEED4, nb_all)
+    lo, hi = shard.block_range_by_bytes(rank, world, q_blocks["len"])
     my = q_blocks[lo:hi].copy()
     base = int(my["off"][0])
     q_host = np.ascontiguousarray(q_src[base:int(my["off"][-1] + my["len"][-1])])
@@ -744,6 +747,60 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
         del e_t, sp_t, d_t, o_t
     if aff0:
         os.sched_setaffinity(0, aff0)
+    return out
+
+
+def leg_host_path_ranks(torch, codec, q, src, enc, eout, enc_bytes, total, n, dev, D, rank, world):
+    """The north-star path at N > 1: each rank decodes its shard of the
+    config-3 batch from pinned host memory through qh_decode_batch(...,
+    QH_WHERE_HOST) -- its own H2D of spans and encoded bytes, its own D2H of
+    the packed decoded bytes, on its own GPU's link (SURVEY.md section
+    8(e)).  Each call is bracketed by barriers and timed as the max over
+    ranks; the median of 5 calls after a warm one.  Aggregate = plaintext of
+    all ranks / that time.  Bit-exact: the packed host output equals the
+    shard's plaintext, which synth lays out back to back in string order."""
+    node, cpus = _gpu_numa(torch, dev)
+    try:
+        aff0 = os.sched_getaffinity(0)
+    except Exception:
+        aff0 = None
+    if cpus and aff0 and cpus & aff0:
+        os.sched_setaffinity(0, cpus & aff0)
+    eo = eout.cpu().numpy()
+    cap_h = int(q.decode_slot_size(eo[:, 1] & 0xFFFFFFFF).sum())
+    e_t = torch.empty(enc_bytes, dtype=torch.uint8, pin_memory=True)
+    e_t.copy_(enc[:enc_bytes])
+    sp_t = torch.zeros(n * 2, dtype=torch.int64, pin_memory=True)
+    spn = sp_t.numpy().view(q.SPAN_IN_DTYPE)
+    spn["off"], spn["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    d_t = torch.empty(max(cap_h, 1), dtype=torch.uint8, pin_memory=True)
+    o_t = torch.empty(n * 2, dtype=torch.int64, pin_memory=True)
+    e_h, d_h, o_h = e_t.numpy(), d_t.numpy(), o_t.numpy().view(q.SPAN_OUT_DTYPE)
+    codec.decode_host(e_h, spn, d_h, o_h)  # warm the staging buffers
+    ts = []
+    for _ in range(5):
+        D.barrier()
+        a = time.perf_counter()
+        codec.decode_host(e_h, spn, d_h, o_h)
+        t = time.perf_counter() - a
+        ts.append((D.max(t), t))
+    ts.sort()
+    t_max, t_mine = ts[2]
+    ok = bool((o_h["status"] == 0).all()) and int(o_h["len"].astype(np.int64).sum()) == total and \
+        bool(np.array_equal(d_h[:total], src[:total].cpu().numpy()))
+    bad = D.sum(0.0 if ok else 1.0)
+    total_all = D.sum(float(total))
+    if aff0:
+        os.sched_setaffinity(0, aff0)
+    out = {"ranks": world, "form": "each rank: its shard, pinned host buffers, own H2D/D2H (qh_decode_batch, "
+                                   "QH_WHERE_HOST)",
+           "plain_bytes_all": int(total_all), "ms_max_over_ranks": round(t_max * 1e3, 2),
+           "decode_GiBps_incl_h2d_d2h_all": round(total_all / t_max / GIB, 2),
+           "ms_each_max_over_ranks": [round(x[0] * 1e3, 2) for x in ts],
+           "ms_rank0": round(t_mine * 1e3, 2) if rank == 0 else None,
+           "gpu_numa_node_rank0": node if rank == 0 else None,
+           "bit_exact": bad == 0}
+    del e_t, sp_t, d_t, o_t
     return out
 
 

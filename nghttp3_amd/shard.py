@@ -77,7 +77,15 @@ def output_offsets(local_bytes: int, dist=None, device=None) -> int:
 
 
 def block_range(rank: int, world: int, nblocks: int):
-    """Config 4: rank's contiguous range of header blocks, [lo, hi).  Blocks
-    at dynamic table 0 are independent, so ranks share nothing but the
-    report (strong scaling over a fixed block count)."""
+    """Rank's contiguous range of nblocks header blocks, [lo, hi), by block
+    count (block_range_by_bytes is what config 4 uses)."""
     return rank * nblocks // world, (rank + 1) * nblocks // world
+
+
+def block_range_by_bytes(rank: int, world: int, block_lens):
+    """Config 4: rank's contiguous range of header blocks, [lo, hi), cut at
+    near-equal block bytes (split_by_bytes over the blocks' lengths: real
+    traffic mixes short and long sections, so a cut by count would leave
+    ranks unequal work).  Blocks at dynamic table 0 are independent, so ranks
+    share nothing but the report (strong scaling over a fixed corpus)."""
+    return split_by_bytes(block_lens, world)[rank]

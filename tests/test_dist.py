@@ -87,7 +87,7 @@ def block_worker(rank, world, port, q):
     try:
         from nghttp3_amd import qpack
         src, blocks, *_ = qpack.synth_field_sections(0x5EED0004, 3001)
-        lo, hi = shard.block_range(rank, world, blocks.size)
+        lo, hi = shard.block_range_by_bytes(rank, world, blocks["len"])
         lines, spans, ls, ss, st = qpack.scan_blocks(src, blocks[lo:hi])
         local = {"blocks": hi - lo, "lines": int(lines.size), "spans": int(spans.size),
                  "errors": int((st != 0).sum()), "time_max": float(rank + 1)}

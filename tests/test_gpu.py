@@ -402,6 +402,54 @@ def test_host_path_multi_context(codec, corpus, digests, nctx):
             c.close()
 
 
+def test_host_path_multi_device(codec, digests):
+    """qh_decode_batch_multi with one context per GPU (devices 0 .. k-1, k <=
+    8): each range's H2D, decode and D2H on its own GPU and link, its host
+    thread making that device current.  Skips on a box with fewer than two
+    GPUs (the driver's node has eight)."""
+    torch = torch_mod()
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("one GPU on this box")
+    from nghttp3_amd import HuffmanBatchCodec
+    d = digests["c3_A"]
+    src, spans, total = codec.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_A)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    e_h = enc[:d["enc_bytes"]].cpu().numpy()
+    eo = eout.cpu().numpy()
+    sp = np.zeros(d["n"], dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    plain = src[:total].cpu().numpy()
+    lens = ln.cpu().numpy()
+    k = min(ndev, 8)
+    codecs = [HuffmanBatchCodec(i, stream=torch.cuda.Stream(device=i)) for i in range(k)]
+    try:
+        dst, out = HuffmanBatchCodec.decode_host_multi(codecs, e_h, sp)
+        assert (out["status"] == 0).all() and (out["len"] == lens).all()
+        got = np.concatenate([dst[o:o + n_] for o, n_ in
+                              zip(out["off"].astype(np.int64), lens.astype(np.int64))])
+        assert got.tobytes() == plain.tobytes()
+    finally:
+        for c in codecs:
+            c.close()
+
+
+def test_host_path_multi_refuses_a_context_twice(codec, corpus):
+    """One thread per context: the same context twice in the list is refused
+    (QH_ERR_INVALID_ARGUMENT) before any work starts."""
+    from nghttp3_amd import HuffmanBatchCodec
+    enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+    sp = np.zeros(len(elen), dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eoff, elen
+    with pytest.raises(Exception) as ei:
+        HuffmanBatchCodec.decode_host_multi([codec, codec], enc, sp)
+    assert "-101" in str(ei.value) or "INVALID" in str(ei.value).upper()
+
+
 def test_host_path_pinned_buffers(codec, corpus, digests):
     """Host-memory decode into pinned dst / out (direct DMA; in development
     builds with QHUFF_HOST_ZC=1 the device-to-host leg as shader stores into

@@ -18,7 +18,7 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 def test_bench_two_ranks_rehearsal():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--one-device", "--strings", "65536", "--steps", "2", "--warmup", "1",
-           "--c5-strings", "200000", "--c4-blocks", "2000", "--no-cpu-baseline", "--no-host-path"]
+           "--c5-strings", "200000", "--c4-blocks", "2000", "--no-cpu-baseline"]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -31,3 +31,10 @@ def test_bench_two_ranks_rehearsal():
     assert ex["config5_zipf"]["bit_exact"] is True and ex["config5_zipf"]["shards"] == 2
     assert ex["config4_qpack_blocks"]["bit_exact"] is True
     assert ex["enc_global_offset_rank0"] == 0
+    # the north-star path at N > 1: every rank its shard from pinned host
+    # memory, timed as the max over ranks, aggregate over all ranks' bytes
+    hp = ex["host_path"]
+    assert hp["ranks"] == 2 and hp["bit_exact"] is True
+    assert hp["plain_bytes_all"] == rec["config"]["plain_bytes_all"]
+    assert hp["decode_GiBps_incl_h2d_d2h_all"] > 0 and hp["ms_rank0"] > 0
+    assert hp["ms_max_over_ranks"] >= hp["ms_rank0"] - 1e-6
