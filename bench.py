@@ -69,6 +69,8 @@ def parse():
                     help="every rank on device 0 (multi-rank rehearsal on a 1-GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the same-run counter passes (rocprofv3 FETCH_SIZE / WRITE_SIZE) and the LDS-chain probe")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the config 4 / config 5 / alphabet-U legs in extra")
     ap.add_argument("--profile-only", action="store_true",
@@ -134,7 +136,7 @@ CHAIN_JSON = os.path.join(ROOT, "profiles", "r03", "lds_chain.json")
 LDS_B32_TBPS = 75.0  # ds_read_b32 aggregate, every CU streaming (MI355X_MICROARCH.md LDS section)
 
 
-def lds_secondary(kernel, avg_us, plain):
+def lds_secondary(kernel, avg_us, plain, chain=None):
     """The decoder's second ceiling: its algorithmic table lookups per
     launch -- one per decoded symbol, the plaintext bytes of this run's batch
     (huffman.c:87-124 makes two per byte of input instead) -- over its time,
@@ -143,17 +145,80 @@ def lds_secondary(kernel, avg_us, plain):
     like the HBM peak) and the guide's ds_read_b32 aggregate."""
     if kernel != "qh_k_dec_peek":
         return None
-    try:
-        chain = json.load(open(CHAIN_JSON))
-    except Exception:
-        return None
+    src = "this run (dev/ubench/lds_chain)"
+    if chain is None:
+        try:
+            chain = json.load(open(CHAIN_JSON))
+            src = "profiles/r03/lds_chain.json"
+        except Exception:
+            return None
     rate = plain / (avg_us * 1e-6)
     agg = LDS_B32_TBPS * 1e12 / 4
     return {"unit": "lookups/s", "lookups_per_launch": int(plain), "achieved": round(rate, -6),
             "chained_rate": chain["chained_lookups_per_s_best"],
             "frac_of_chained_rate": round(rate / chain["chained_lookups_per_s_best"], 4),
             "ds_read_b32_aggregate": agg, "frac_of_aggregate": round(rate / agg, 4),
-            "source": "lookups: decoded symbols of this run; chained rate: profiles/r03/lds_chain.json"}
+            "source": "lookups: decoded symbols of this run; chained rate: " + src}
+
+
+def leg_counters(args, kernel="qh_k_dec_peek"):
+    """Same-run evidence for the roofline: two rocprofv3 counter passes over a
+    profile-only child of this bench (config 3, the same batch and library:
+    FETCH_SIZE alone, then WRITE_SIZE alone -- gfx950 collects one TCC group
+    per pass), each under its own time limit, from /tmp (MI355X_MICROARCH.md
+    HBM section: FETCH_SIZE counts 64-byte requests where wide reads are 128
+    bytes, so it is doubled; both in KiB), and the dependent-LDS-lookup
+    ceiling from dev/ubench/lds_chain on this box.  The child is a process of
+    its own (rocprofv3 -- python3 ...), started before nothing but a fork."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    out = {"kernel": kernel}
+    chain = None
+    exe = os.path.join(ROOT, "dev", "ubench", "lds_chain")
+    if os.path.exists(exe):
+        try:
+            r = subprocess.run([exe], capture_output=True, text=True, timeout=90)
+            js = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode == 0 and js:
+                chain = json.loads(js[-1])
+        except Exception as e:  # (reported, not fatal)
+            out["lds_chain_error"] = str(e)[:200]
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="qh_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, ctr)
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--profile-only", "--steps", "3", "--warmup", "1",
+               "--strings", str(args.strings), "--min-len", str(args.min_len), "--max-len", str(args.max_len),
+               "--alphabet", args.alphabet, "--seed", hex(args.seed)]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd="/tmp", env=env)
+        except subprocess.TimeoutExpired:
+            out["error"] = f"{ctr} pass timed out"
+            break
+        xs = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    name = row.get("Kernel_Name", "")
+                    if kernel in name and row.get("Counter_Name") == ctr:
+                        xs.append(float(row["Counter_Value"]))
+        if r.returncode != 0 or not xs:
+            out["error"] = f"{ctr} pass rc={r.returncode}, {len(xs)} rows: " + r.stderr[-300:]
+            break
+        vals[ctr] = sum(xs) / len(xs)
+        out[ctr.lower() + "_launches"] = len(xs)
+    shutil.rmtree(tmp, ignore_errors=True)
+    if len(vals) == 2:
+        out["fetch_bytes"] = round(2 * 1024 * vals["FETCH_SIZE"])
+        out["write_bytes"] = round(1024 * vals["WRITE_SIZE"])
+        out["hbm_bytes_per_launch"] = out["fetch_bytes"] + out["write_bytes"]
+        out["correction"] = "FETCH_SIZE x2 (gfx950 128-byte requests counted as 64); KiB -> bytes"
+    return out, chain
 
 
 def _cpu_model():
@@ -299,8 +364,12 @@ def main():
     kern = kernel_table(ktimes, n, total, enc_bytes)
     dom = max(kern, key=lambda k: kern[k]["avg_us"] * kern[k]["launches"]) if kern else None
     traffic = None
+    counters, chain = None, None
+    if rank == 0 and world == 1 and dom and not args.no_pmc:
+        counters, chain = leg_counters(args, dom)
+        traffic = counters.get("hbm_bytes_per_launch")
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if dom and os.path.exists(pmc_path):
+    if traffic is None and dom and os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             entry = pmc.get("kernels", {}).get(dom)
@@ -314,8 +383,13 @@ def main():
         roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "algo_bytes_per_launch": kern[dom]["algo_bytes"],
-                    "avg_us": kern[dom]["avg_us"]}
-        sec = lds_secondary(dom, kern[dom]["avg_us"], total)
+                    "avg_us": kern[dom]["avg_us"],
+                    "traffic_source": ("this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                       "(extra.counters)" if counters and counters.get("hbm_bytes_per_launch")
+                                       else "profiles/pmc_traffic.json" if traffic else None)}
+        if traffic:
+            roofline["traffic_over_algo"] = round(traffic / max(kern[dom]["algo_bytes"] or 1, 1), 3)
+        sec = lds_secondary(dom, kern[dom]["avg_us"], total, chain)
         if sec:
             roofline["secondary"] = sec
             if sec["frac_of_chained_rate"] > roofline["frac"]:
@@ -473,7 +547,7 @@ def main():
                       "decode_dense_GiBps": round(total_all / t_dense / GIB, 2),
                       "decode_dense_bit_exact": dense_ok,
                       "enc_global_offset_rank0": enc_global_off,
-                      "kernels": kern, "host_path": host_path,
+                      "kernels": kern, "host_path": host_path, "counters": counters,
                       "config5_zipf": config5, "config4_qpack_blocks": config4,
                       "config1_qif": config1,
                       "config3_alphabet_U": configU},
