@@ -161,7 +161,7 @@ def lds_secondary(kernel, avg_us, plain, chain=None):
             "source": "lookups: decoded symbols of this run; chained rate: " + src}
 
 
-def leg_counters(args, kernel="qh_k_dec_peek"):
+def leg_counters(args, kernel="qh_k_dec_peek", coalesced=None):
     """Same-run evidence for the roofline: two rocprofv3 counter passes over a
     profile-only child of this bench (config 3, the same batch and library:
     FETCH_SIZE alone, then WRITE_SIZE alone -- gfx950 collects one TCC group
@@ -169,7 +169,16 @@ def leg_counters(args, kernel="qh_k_dec_peek"):
     HBM section: FETCH_SIZE counts 64-byte requests where wide reads are 128
     bytes, so it is doubled; both in KiB), and the dependent-LDS-lookup
     ceiling from dev/ubench/lds_chain on this box.  The child is a process of
-    its own (rocprofv3 -- python3 ...), started before nothing but a fork."""
+    its own (rocprofv3 -- python3 ...), started before nothing but a fork.
+
+    FETCH_SIZE is calibrated per access pattern (dev/ubench/rd_gran.hip,
+    profiles/r05/rd_gran_fetch.txt: 256 MiB read once): coalesced 16-byte
+    lane loads report 0.50 of the bytes (the guide's x2), but per-lane
+    16-byte loads walking separate regions -- the decoder's input DMAs and
+    string-start loads -- report 1.06 of them (each 64-byte request counted
+    whole).  So with `coalesced` = the kernel's bytes read by coalesced loads
+    (the decoder's spans, 16 N), fetch = raw + coalesced / 2; without it, the
+    guide's x2."""
     import csv
     import glob
     import shutil
@@ -214,10 +223,17 @@ def leg_counters(args, kernel="qh_k_dec_peek"):
         out[ctr.lower() + "_launches"] = len(xs)
     shutil.rmtree(tmp, ignore_errors=True)
     if len(vals) == 2:
-        out["fetch_bytes"] = round(2 * 1024 * vals["FETCH_SIZE"])
+        raw = 1024 * vals["FETCH_SIZE"]
+        out["fetch_raw_bytes"] = round(raw)
+        if coalesced is not None:
+            out["fetch_bytes"] = round(raw + coalesced / 2)
+            out["correction"] = (f"FETCH_SIZE calibrated per pattern (dev/ubench/rd_gran): per-lane 16-byte loads "
+                                 f"x1, the {coalesced} bytes of coalesced span loads x2; KiB -> bytes")
+        else:
+            out["fetch_bytes"] = round(2 * raw)
+            out["correction"] = "FETCH_SIZE x2 (guide: coalesced wide reads; this kernel uncalibrated); KiB -> bytes"
         out["write_bytes"] = round(1024 * vals["WRITE_SIZE"])
         out["hbm_bytes_per_launch"] = out["fetch_bytes"] + out["write_bytes"]
-        out["correction"] = "FETCH_SIZE x2 (gfx950 128-byte requests counted as 64); KiB -> bytes"
     return out, chain
 
 
@@ -366,7 +382,7 @@ def main():
     traffic = None
     counters, chain = None, None
     if rank == 0 and world == 1 and dom and not args.no_pmc:
-        counters, chain = leg_counters(args, dom)
+        counters, chain = leg_counters(args, dom, 16 * n if dom == "qh_k_dec_peek" else None)
         traffic = counters.get("hbm_bytes_per_launch")
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if traffic is None and dom and os.path.exists(pmc_path):

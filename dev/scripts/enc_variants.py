@@ -3,6 +3,7 @@
 check their bytes agree (development tool, one GPU).
 Usage: python scripts/enc_variants.py [--n N] [--alphabet A|U] [--zipf]"""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -60,7 +61,9 @@ def main():
         print(json.dumps({"encoder": kind, "alphabet": args.alphabet, "zipf": args.zipf, "n": n,
                           "kernels_us": ks, "sum_us": round(sum(ks.values()), 2), "wall_us": round(wall_us, 2),
                           "plain_GiBps": round(total / (sum(ks.values()) * 1e-6) / 2**30, 1),
-                          "same_as_windows": same}), flush=True)
+                          "same_as_windows": same,
+                          "sha": hashlib.sha256(got[0].cpu().numpy().tobytes() + got[1].cpu().numpy().tobytes())
+                          .hexdigest()[:16]}), flush=True)
 
 
 if __name__ == "__main__":
