@@ -141,3 +141,10 @@ ew3: $(LIBDIR)/libqhuff_ew3.so
 $(LIBDIR)/libqhuff_ew3.so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_EW_MIN_WAVES=0 -c $< -o $(LIBDIR)/qh_device_ew3.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_ew3.o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# Framing count pass with FRC blocks per wave (development timing:
+# make frc FRC=16|32) -> libqhuff_frc<FRC>.so
+frc: $(LIBDIR)/libqhuff_frc$(FRC).so
+$(LIBDIR)/libqhuff_frc$(FRC).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_FR_COUNT=$(FRC) -c $< -o $(LIBDIR)/qh_device_frc$(FRC).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frc$(FRC).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

@@ -23,6 +23,8 @@ LAYOUT = {
     "enc_lens": ({0: "head", 2: "dma wait", 3: "lookups", 4: "scan", 5: "ends", 6: "tail"},
                  10, 10, 11),
     "enc_lanes": ({0: "setup", 1: "encode", 2: "copy-out"}, 10, 10, None),
+    "encs": ({0: "front setup", 1: "count loop", 2: "count tail", 3: "look-back", 4: "lookups+ends",
+              5: "byte chain", 6: "flush", 10: "merge"}, 11, 11, None),
 }
 
 
@@ -58,11 +60,14 @@ def main():
         "dec_peek": lambda: codec.decode_dev(enc, eout, dec, dout),
         "enc_lens": lambda: codec.encode_count_dev(src, spans, hlen),
         "enc_lanes": lambda: codec.encode_dev(src, spans, enc, eout),
+        "encs": lambda: codec.encode_dev(src, spans, enc, eout),
     }
     only = os.environ.get("KERNELS")
     for kern, fn in runs.items():
         if only and kern not in only.split(","):
             continue
+        if kern == "encs":
+            codec.set_encoder("fused")
         for _ in range(reps):
             fn()
         codec.sync()

@@ -54,7 +54,9 @@
 #include "qh_lut_dec.inc"    // decoder: 12-bit table, one string per lane
 #endif
 #include "qh_peek_dec.inc"   // decoders (windows: default; waves): W-bit peek table + leading-ones table
-#include "qh_pair_dec.inc"   // decoder: two codes per lookup, waves fed from a group queue
+#ifdef QH_DEV_VARIANTS
+#include "qh_pair_dec.inc"   // (dev/csrc) decoder: two codes per lookup, waves fed from a group queue
+#endif
 #ifdef QH_DEV_VARIANTS
 #include "qh_dec3.inc"       // decoder: plan + task-queue lanes
 #endif
@@ -65,6 +67,7 @@
 #include "qh_enc_waves.inc"   // encoder codes (QH_ENCODER_WAVES): per-wave chunks, LDS rings
 #include "qh_enc_fused.inc"   // encoder, lengths + codes in one pass (QH_ENCODER_FUSED)
 #ifdef QH_DEV_VARIANTS
+#include "qh_enc_seg.inc"    // (dev/csrc) encoder, one pass over equal-size segments per lane
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
 #endif
 #include "qh_synth.inc"      // synthetic inputs for bench/tests
