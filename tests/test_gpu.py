@@ -1127,3 +1127,75 @@ def test_encoder_variants(kind, corpus, kat, digests):
         assert sha(encu[:d["enc_bytes"]].cpu().numpy()) == d["enc_sha256"]
     finally:
         c.close()
+
+
+@pytest.mark.gpu
+def test_cu_masked_stream_fallbacks(corpus):
+    """A context on a stream whose CU mask leaves out most of the chip
+    (hipExtStreamCreateWithCUMask, 96 of 256 CUs: some XCDs get no wave)
+    takes the one-ticket-counter forms of the fused encoder and the framing
+    count (qh_api.inc stream_all_cus): their results equal the full-chip
+    context's."""
+    import ctypes
+    from nghttp3_amd import HuffmanBatchCodec, qpack
+    torch = torch_mod()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint32)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    mask = (ctypes.c_uint32 * 8)(0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0, 0, 0, 0, 0)
+    stream = ctypes.c_void_p()
+    assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(stream), 8, mask) == 0
+    # the library's test (stream_all_cus): the stream's mask, as HIP reports it,
+    # must not cover every CU
+    hip.hipExtStreamGetCUMask.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    got_mask = (ctypes.c_uint32 * 8)()
+    assert hip.hipExtStreamGetCUMask(stream, 8, got_mask) == 0
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert 0 < sum(bin(x).count("1") for x in got_mask) < ncu
+    full = HuffmanBatchCodec(device=0)
+    part = HuffmanBatchCodec(device=0, stream=stream.value)
+    try:
+        # the fused encoder: corpus strings and a 300k-string synthetic batch
+        n = len(corpus["len"])
+        srcd = to_dev(corpus["plain"])
+        spd = spans_dev(corpus["off"], corpus["len"])
+        cases = [(srcd, spd, n)]
+        s2, sp2, _ = full.synth(0x5EED00C0, 300000, 1, 300, synth.ALPHABET_A)
+        cases.append((s2, sp2, 300000))
+        for src, sp, m in cases:
+            ln = (sp[:, 1] & 0xFFFFFFFF).cpu().numpy().astype(np.int64)
+            bound = int(((ln * 30 + 7) // 8).sum()) + 16
+            res = []
+            for c in (full, part):
+                c.set_encoder("fused")
+                dst = torch.zeros(bound, dtype=torch.uint8, device="cuda")
+                out = torch.zeros((m, 2), dtype=torch.int64, device="cuda")
+                torch.cuda.synchronize()
+                c.encode_dev(src, sp, dst, out)
+                c.sync()
+                torch.cuda.synchronize()
+                res.append((dst.cpu().numpy(), out.cpu().numpy()))
+            assert np.array_equal(res[0][1], res[1][1])
+            assert np.array_equal(res[0][0], res[1][0])
+            o, l, s = q.unpack_out(torch.from_numpy(res[1][1]))
+            assert (s == 0).all()
+        # framing (qh_k_frame_count's tickets) through the sections decoder
+        src, blocks, *_ = qpack.synth_field_sections(0x5EED0004, 20000)
+        d_src = torch.from_numpy(np.ascontiguousarray(src)).cuda()
+        d_blk = torch.from_numpy(blocks.view(np.int64).reshape(-1, 2).copy()).cuda()
+        got = []
+        for c in (full, part):
+            torch.cuda.synchronize()
+            b = qpack.FieldSectionDecoder(codec=c, dtable0=True).decode_blocks_dev(d_src, d_blk)
+            c.sync()
+            torch.cuda.synchronize()
+            ns, nl = int(b["nspans"]), int(b["nlines"])
+            got.append((b["strs"][:ns].cpu().numpy().tobytes(), b["spans"][:ns].cpu().numpy().tobytes(),
+                        b["lines"][:nl * 24].cpu().numpy().tobytes(), b["verdict"][:ns].cpu().numpy().tobytes(),
+                        b["status"][:20000].cpu().numpy().tobytes(), ns, nl))
+        assert got[0][5] > 0 and got[0] == got[1]
+    finally:
+        part.close()
+        full.close()
+        hip.hipStreamDestroy(stream)
