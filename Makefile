@@ -148,3 +148,10 @@ frc: $(LIBDIR)/libqhuff_frc$(FRC).so
 $(LIBDIR)/libqhuff_frc$(FRC).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_FR_COUNT=$(FRC) -c $< -o $(LIBDIR)/qh_device_frc$(FRC).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_frc$(FRC).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# Codes-pass occupancy variants (development timing: make encw5 EW=<waves>
+# ES=<stage bytes>) -> libqhuff_ew<EW>s<ES>.so
+encw5: $(LIBDIR)/libqhuff_ew$(EW)s$(ES).so
+$(LIBDIR)/libqhuff_ew$(EW)s$(ES).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) -DQH_ENC_WAVES=$(EW) -DQH_ENC_STAGE=$(ES) -c $< -o $(LIBDIR)/qh_device_ew$(EW)s$(ES).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_ew$(EW)s$(ES).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
