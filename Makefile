@@ -155,3 +155,9 @@ encw5: $(LIBDIR)/libqhuff_ew$(EW)s$(ES).so
 $(LIBDIR)/libqhuff_ew$(EW)s$(ES).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
 	$(HIPCC) $(HIPFLAGS) -DQH_ENC_WAVES=$(EW) -DQH_ENC_STAGE=$(ES) -c $< -o $(LIBDIR)/qh_device_ew$(EW)s$(ES).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_ew$(EW)s$(ES).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+
+# a build with extra defines: make var V=<name> D="-DQH_...=..."
+var: $(LIBDIR)/libqhuff_v$(V).so
+$(LIBDIR)/libqhuff_v$(V).so: $(CSRC)/qh_device.hip $(CSRC)/*.inc $(CSRC)/qh_common.h $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o
+	$(HIPCC) $(HIPFLAGS) $(D) -c $< -o $(LIBDIR)/qh_device_v$(V).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIBDIR)/qh_device_v$(V).o $(LIBDIR)/qh_scalar.o $(LIBDIR)/qh_qpack.o $(LIBDIR)/qh_http.o $(LIBDIR)/qh_static.o

@@ -51,8 +51,11 @@ SEED5, SEED4 = 0x5EED0005, 0x5EED0004
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # (200 steps: the timed region's fixed cost -- the first launch after the
+    # synchronize and the closing synchronize, ~0.3 ms -- is 4.5% of 20
+    # round trips and 0.5% of 200; dev/scripts/step_host.py)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     # (no option may be a prefix of a torch.distributed.run option: --n, --lo ...)
     ap.add_argument("--strings", type=int, default=1 << 20, help="strings per GPU (config 3)")
     ap.add_argument("--min-len", type=int, default=8)
