@@ -5,7 +5,7 @@ i=0
 for E in $2; do
 i=$((i+1))
 EV=""; [ "$E" != base ] && EV=$(echo $E | tr ',' ' ')
-env $EV timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-host-path --no-pmc --no-configs --steps 40 > $O/b$i.json 2> $O/b$i.err || { tail -5 $O/b$i.err; exit 1; }
+env $EV timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-host-path --no-pmc --no-configs > $O/b$i.json 2> $O/b$i.err || { tail -5 $O/b$i.err; exit 1; }
 python -c "
 import json,sys;d=json.loads(open('$O/b$i.json').read().strip().splitlines()[-1])
 k=d['extra']['kernels']; print('$E', d['value'], d['ms_per_step'], {n: v['avg_us'] for n,v in k.items()})"
