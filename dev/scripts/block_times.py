@@ -30,6 +30,7 @@ def main():
     dec = torch.empty(cap + 64, dtype=torch.uint8, device="cuda")
     dout = torch.empty((n, 2), dtype=torch.int64, device="cuda")
     run = {"enc_lens": lambda: codec.encode_count_dev(src, spans, hlen),
+           "enc": lambda: codec.encode_dev(src, spans, enc, eout),  # (the codes pass's blocks: it runs last)
            "dec": lambda: codec.decode_dev(enc, eout, dec, dout)}[which]
     for _ in range(3):
         run()
