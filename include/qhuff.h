@@ -206,6 +206,19 @@ QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
 #define QH_ENCODER_FUSED 2
 #define QH_ENCODER_AUTO 3
 QH_EXPORT int qh_ctx_set_encoder(qh_ctx *ctx, int kind);
+/* Tuning options (results are identical; speed is not).  The library reads
+ * no environment variable that changes what it computes or which kernels
+ * run: these are set explicitly, per context.
+ * QH_OPT_LONG_MIN: QH_DECODER_SORTED decodes strings of at least `value`
+ *   encoded bytes (their 16-byte length class and longer) with a workgroup
+ *   per string; 0 turns that path off (default 4096; at most 2^30).
+ * QH_OPT_LENS_LANE_PASS: 1 counts every string's encoded length a lane per
+ *   string (the path the length kernel takes for scattered spans) instead
+ *   of streaming the strings' region; 0 (default) chooses per window.
+ * No reference counterpart (the reference codec has no batch kernels). */
+#define QH_OPT_LONG_MIN 1
+#define QH_OPT_LENS_LANE_PASS 2
+QH_EXPORT int qh_ctx_set_option(qh_ctx *ctx, int option, int64_t value);
 QH_EXPORT void *qh_ctx_stream(qh_ctx *ctx);
 /* Wait for all work queued on the context's stream. */
 QH_EXPORT int qh_ctx_sync(qh_ctx *ctx);

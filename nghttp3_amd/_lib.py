@@ -31,6 +31,8 @@ QH_ENCODER_WINDOWS = 0
 QH_ENCODER_WAVES = 1
 QH_ENCODER_FUSED = 2
 QH_ENCODER_AUTO = 3
+QH_OPT_LONG_MIN = 1
+QH_OPT_LENS_LANE_PASS = 2
 
 NGHTTP3_QPACK_HUFFMAN_FLAG_ACCEPTED = 0x01
 NGHTTP3_QPACK_HUFFMAN_FLAG_SYM = 0x02
@@ -92,6 +94,7 @@ EXPORTED_FUNCTIONS = (
     "qh_ctx_set_stream",
     "qh_ctx_set_decoder",
     "qh_ctx_set_encoder",
+    "qh_ctx_set_option",
     "qh_ctx_stream",
     "qh_ctx_sync",
     "qh_ctx_last_stats",
@@ -176,6 +179,8 @@ def load():
     lib.qh_ctx_set_decoder.restype = i32
     lib.qh_ctx_set_encoder.argtypes = [vp, i32]
     lib.qh_ctx_set_encoder.restype = i32
+    lib.qh_ctx_set_option.argtypes = [vp, i32, ctypes.c_int64]
+    lib.qh_ctx_set_option.restype = i32
     lib.qh_ctx_set_stream.argtypes = [vp, vp]
     lib.qh_ctx_set_stream.restype = i32
     lib.qh_ctx_stream.argtypes = [vp]

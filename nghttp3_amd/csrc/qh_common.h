@@ -4,6 +4,20 @@
 
 namespace qhk {
 
+// Development knobs -- the QHUFF_* environment variables other than
+// QHUFF_VERBOSE, and the kernels' store probes (QHUFF_DEBUG bits that skip or
+// misplace output stores) -- exist only in development builds (make dev,
+// make stamps, make var ...).  The product library's output never depends on
+// its environment, as the reference codec's does not (huffman.c:87-124).
+#if defined(QH_DEV_VARIANTS) || defined(QH_STAMPS) || defined(QH_DEV_KNOBS_ON)
+#define QH_DEV_KNOBS 1
+#else
+#define QH_DEV_KNOBS 0
+#endif
+// A development probe bit of a kernel's dbg word: constant false in the
+// product build, so the probe's branch compiles out.
+#define QH_PROBE(d, bits) (QH_DEV_KNOBS && ((d) & (bits)) != 0u)
+
 // Phase timers for kernel development (make stamps -> libqhuff_stamps.so):
 // wave 0 of every workgroup adds s_memtime deltas per phase slot.  Compiled
 // out of the product library.

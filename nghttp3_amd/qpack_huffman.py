@@ -183,6 +183,14 @@ class HuffmanBatchCodec:
              "fused": _lib.QH_ENCODER_FUSED, "auto": _lib.QH_ENCODER_AUTO}[kind]
         _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")
 
+    def set_option(self, option: str, value: int):
+        """Tuning options (include/qhuff.h QH_OPT_*; results are identical):
+        'long_min' (the sorted decoder's workgroup-per-string threshold, in
+        encoded bytes; 0 = off) and 'lens_lane_pass' (1: every string's
+        encoded length counted a lane per string)."""
+        k = {"long_min": _lib.QH_OPT_LONG_MIN, "lens_lane_pass": _lib.QH_OPT_LENS_LANE_PASS}[option]
+        _lib.check(self._lib.qh_ctx_set_option(self._ctx, k, int(value)), "qh_ctx_set_option")
+
     def sync(self):
         _lib.check(self._lib.qh_ctx_sync(self._ctx), "qh_ctx_sync")
 

@@ -94,3 +94,15 @@ def test_c_program_links_static_archive_in_place_of_reference_objects(tmp_path):
                            str(src), archive, "-L/opt/rocm/lib", "-lamdhip64", "-lstdc++",
                            "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)])
     assert subprocess.check_output([str(exe)], text=True).strip() == "ok"
+
+
+def test_product_library_reads_no_development_knob():
+    """The shipped libqhuff.so holds no development environment knob: the
+    only QHUFF_* string is QHUFF_VERBOSE (a stderr report of the kernels'
+    occupancy).  Tuning goes through qh_ctx_set_option; results never depend
+    on the environment (the reference codec is pure,
+    huffman.c:87-124)."""
+    from nghttp3_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    found = set(m.decode() for m in re.findall(rb"QHUFF_[A-Z0-9_]+", data))
+    assert found <= {"QHUFF_VERBOSE"}, found

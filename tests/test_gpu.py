@@ -574,6 +574,58 @@ def _full_size_config(codec, digests, name):
     assert bool((dec[rep_d + pos] == src[:total]).all())
 
 
+_ENV_PROBE = r"""
+import hashlib, json, sys
+import torch
+from nghttp3_amd import HuffmanBatchCodec, synth
+d = json.loads(sys.argv[1])
+c = HuffmanBatchCodec(device=0)
+src, spans, total = c.synth(d["seed"], d["n"], d["lo"], d["hi"], synth.ALPHABET_A)
+ln = spans[:, 1] & 0xFFFFFFFF
+enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+eout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+c.encode_dev(src, spans, enc, eout)
+elen = eout[:, 1] & 0xFFFFFFFF
+cap = int(((elen * 8 // 5 + 16 + 63) // 64 * 64).sum().item())
+dec = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+dout = torch.zeros((d["n"], 2), dtype=torch.int64, device="cuda")
+c.decode_dev(enc, eout, dec, dout)
+st = c.stats()
+dlen = dout[:, 1] & 0xFFFFFFFF
+rep_d = torch.repeat_interleave(dout[:, 0], ln)
+pos = torch.arange(total, device="cuda", dtype=torch.int64) - torch.repeat_interleave(spans[:, 0], ln)
+print(json.dumps({
+    "enc_sha256": hashlib.sha256(enc[:d["enc_bytes"]].cpu().numpy().tobytes()).hexdigest(),
+    "dec_ok": bool((dlen == ln).all()) and bool((dec[rep_d + pos] == src[:total]).all()),
+    "errors": int(st["n_errors"])}))
+"""
+
+
+def test_results_ignore_environment(digests):
+    """The product library reads no development knob from the environment
+    (QHUFF_DEBUG bits used to skip or misplace the decoder's
+    stores with every status 0): a fresh process with every former knob set
+    to a hostile value still encodes config 3 to the oracle's digest and
+    decodes it back bit-exact (the reference codec is pure,
+    huffman.c:87-124)."""
+    import json
+    import subprocess
+    import sys
+    d = digests["c3_A"]
+    env = dict(os.environ)
+    env.update({"QHUFF_DEBUG": "0x1F", "QHUFF_DECODER": "bogus", "QHUFF_CODES": "fused",
+                "QHUFF_LONG_MIN": "1", "QHUFF_PLAN_SKEW": "nan", "QHUFF_PLAN_SKEW_LONG": "-1",
+                "QHUFF_BPC": "64", "QHUFF_ENC_BPC": "64", "QHUFF_ENC_THREADS": "128",
+                "QHUFF_SEG": "1", "QHUFF_LENS_WIN64": "1", "QHUFF_HOST_MAPPED_ENDS": "1"})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ENV_PROBE, json.dumps(d)], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "not a decoder" not in r.stderr  # (QHUFF_DECODER is not even read)
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got == {"enc_sha256": d["enc_sha256"], "dec_ok": True, "errors": 0}
+
+
 def test_window_decoder_plan_mixed_blocks(codec, corpus):
     """The window decoder's per-block plan (qh_k_dec_plan): a batch whose
     first half has 8-256 B lengths (blocks decoded from their windows of
@@ -962,7 +1014,7 @@ def test_long_strings_wave_per_string(alphabet, decoder):
     start at 16-byte boundaries and resynchronise) on strings of 4-40 KB --
     the sorted decoder's longest class, the window decoder's deferred
     strings -- and on strings of 200-3000 B with the sorted decoder's
-    threshold lowered (QHUFF_LONG_MIN) so that both paths run in one batch:
+    threshold lowered (qh_ctx_set_option QH_OPT_LONG_MIN) so that both paths run in one batch:
     statuses, lengths and bytes as the oracle's."""
     from nghttp3_amd import HuffmanBatchCodec
     rng = np.random.default_rng(0x10A9 + (alphabet == "U"))
@@ -970,16 +1022,9 @@ def test_long_strings_wave_per_string(alphabet, decoder):
     cases = [(None, _long_strings(rng, 96, alph, 4096, 40000)),
              ("300", _long_strings(rng, 600, alph, 200, 3000) + _long_strings(rng, 40, alph, 1, 64))]
     for long_min, strs in cases:
-        old = os.environ.get("QHUFF_LONG_MIN")
+        c = HuffmanBatchCodec(device=0)
         if long_min is not None:
-            os.environ["QHUFF_LONG_MIN"] = long_min
-        try:
-            c = HuffmanBatchCodec(device=0)
-        finally:
-            if old is None:
-                os.environ.pop("QHUFF_LONG_MIN", None)
-            else:
-                os.environ["QHUFF_LONG_MIN"] = old
+            c.set_option("long_min", int(long_min))
         try:
             c.set_decoder(decoder)
             order = rng.permutation(len(strs))
@@ -1001,23 +1046,14 @@ def test_long_strings_wave_per_string(alphabet, decoder):
 def test_encode_length_passes(mode, corpus, digests):
     """The encoder's passes: streaming lengths + lane-per-string codes
     (default), and every window's lengths counted a lane per string inside
-    the length kernel (QHUFF_DEBUG=4, the scattered-window path) -- corpus
+    the length kernel (QH_OPT_LENS_LANE_PASS, the scattered-window path) -- corpus
     lengths/codes, counts, overlapping and scattered spans, and the
     full-size c2_U digest."""
     import os
     from nghttp3_amd import HuffmanBatchCodec
-    env = {"default": {}, "lane": {"QHUFF_DEBUG": "4"}}[mode]
-    old = {k: os.environ.get(k) for k in ("QHUFF_DEBUG",)}
-    for k in old:
-        os.environ.pop(k, None)
-    os.environ.update(env)
-    try:
-        c = HuffmanBatchCodec(device=0)
-    finally:
-        for k, v in old.items():
-            os.environ.pop(k, None)
-            if v is not None:
-                os.environ[k] = v
+    c = HuffmanBatchCodec(device=0)
+    if mode == "lane":
+        c.set_option("lens_lane_pass", 1)
     try:
         torch = torch_mod()
         test_corpus_encode(c, corpus)
