@@ -205,6 +205,12 @@ QH_EXPORT int qh_ctx_set_decoder(qh_ctx *ctx, int kind);
  * output, and the codes go out through an LDS stage. */
 #define QH_ENCODER_FUSED 2
 #define QH_ENCODER_AUTO 3
+/* QH_ENCODER_REGION: the length pass, then a codes pass that streams the
+ * plaintext region of every 64 strings lying back to back in memory (lane j
+ * of a wave: bytes [16 j, 16 j + 16) of each 1 KiB round, codes placed by a
+ * prefix sum of their lengths and the strings' pads); strings in any other
+ * layout a lane each.  QH_ENCODER_AUTO's choice for header text. */
+#define QH_ENCODER_REGION 4
 QH_EXPORT int qh_ctx_set_encoder(qh_ctx *ctx, int kind);
 /* Tuning options (results are identical; speed is not).  The library reads
  * no environment variable that changes what it computes or which kernels

@@ -31,6 +31,7 @@ QH_ENCODER_WINDOWS = 0
 QH_ENCODER_WAVES = 1
 QH_ENCODER_FUSED = 2
 QH_ENCODER_AUTO = 3
+QH_ENCODER_REGION = 4
 QH_OPT_LONG_MIN = 1
 QH_OPT_LENS_LANE_PASS = 2
 

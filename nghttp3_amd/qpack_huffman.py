@@ -180,7 +180,8 @@ class HuffmanBatchCodec:
         (strings of similar length), 'waves' or 'fused' (one pass: long,
         skewed or binary strings); results are identical."""
         k = {"windows": _lib.QH_ENCODER_WINDOWS, "waves": _lib.QH_ENCODER_WAVES,
-             "fused": _lib.QH_ENCODER_FUSED, "auto": _lib.QH_ENCODER_AUTO}[kind]
+             "fused": _lib.QH_ENCODER_FUSED, "auto": _lib.QH_ENCODER_AUTO,
+             "region": _lib.QH_ENCODER_REGION}[kind]
         _lib.check(self._lib.qh_ctx_set_encoder(self._ctx, k), "qh_ctx_set_encoder")
 
     def set_option(self, option: str, value: int):

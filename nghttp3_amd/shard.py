@@ -87,5 +87,13 @@ def block_range_by_bytes(rank: int, world: int, block_lens):
     near-equal block bytes (split_by_bytes over the blocks' lengths: real
     traffic mixes short and long sections, so a cut by count would leave
     ranks unequal work).  Blocks at dynamic table 0 are independent, so ranks
-    share nothing but the report (strong scaling over a fixed corpus)."""
-    return split_by_bytes(block_lens, world)[rank]
+    share nothing but the report (strong scaling over a fixed corpus).
+
+    A cut by bytes can leave a rank no block (one block larger than a
+    rank's share); every rank then takes the cut by count instead, so no
+    rank has an empty range while world <= len(block_lens)."""
+    ranges = split_by_bytes(block_lens, world)
+    n = len(block_lens)
+    if world <= n and any(b == e for b, e in ranges):
+        return block_range(rank, world, n)
+    return ranges[rank]

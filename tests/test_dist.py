@@ -118,3 +118,20 @@ def test_sharded_blocks_gloo():
     assert rep == res[1][3]
     assert rep["blocks"] == blocks.size and rep["lines"] == lines.size
     assert rep["spans"] == spans.size and rep["errors"] == 0 and rep["time_max"] == world
+
+
+def test_block_range_by_bytes_never_empty():
+    """A block bigger than a rank's byte share would leave a later rank no
+    block under the byte cut; the split then falls back to the count cut, so
+    every rank of a world <= nblocks has at least one block and the ranges
+    tile [0, nblocks) (my["off"][0] on an empty range)."""
+    lens = np.array([10_000] + [10] * 7, dtype=np.uint64)
+    for world in range(1, 9):
+        rs = [shard.block_range_by_bytes(r, world, lens) for r in range(world)]
+        assert rs[0][0] == 0 and rs[-1][1] == lens.size
+        assert all(lo < hi for lo, hi in rs), (world, rs)
+        assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+    # balanced blocks keep the byte cut
+    even = np.full(64, 100, dtype=np.uint64)
+    assert [shard.block_range_by_bytes(r, 4, even) for r in range(4)] == \
+        [(0, 16), (16, 32), (32, 48), (48, 64)]

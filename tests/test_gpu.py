@@ -522,13 +522,14 @@ def test_synth_device_matches_host(codec):
                                           ("c3_A", "windows"), ("c3_A", "waves"),
                                           ("c2_U", "waves"), ("c3_A", "fused"),
                                           ("c2_U", "fused"), ("c3_A", "sorted"),
-                                          ("c2_U", "sorted")])
+                                          ("c2_U", "sorted"), ("c2_A", "region"),
+                                          ("c3_A", "region"), ("c2_U", "region")])
 def test_full_size_config(codec, digests, name, decoder):
     """BASELINE configs at full size (2^20 strings): synth digest, encode
     digest vs the oracle's, then decode round trip (size-independent), with
     either shipped decoder ("fused": the fused encoder, window decoder;
     "sorted": the window encoder, the sorted decoder)."""
-    codec.set_decoder(decoder if decoder != "fused" else "windows")
+    codec.set_decoder(decoder if decoder not in ("fused", "region") else "windows")
     codec.set_encoder(decoder if decoder != "sorted" else "windows")
     try:
         _full_size_config(codec, digests, name)
@@ -670,15 +671,17 @@ def test_window_decoder_plan_mixed_blocks(codec, corpus):
         assert dst[o[i]:o[i] + l[i]].tobytes() == want_dst[int(want_slot[i]):int(want_slot[i]) + int(l[i])].tobytes(), i
 
 
-@pytest.mark.parametrize("decoder", ["windows", "waves", "sorted"])
+@pytest.mark.parametrize("decoder", ["windows", "waves", "sorted", "region"])
 def test_config5_rank_shard_full_size(codec, digests, decoder):
     """Config 5 at size: rank 0's shard of 16M Zipf strings split by bytes
     over 8 GPUs (2.1M strings, 438 MB, lengths 1..4096), as bench.py cuts
     it: the device generator from the global byte offset, encode digests vs
     the oracle's, then the decode round trip (chunked compare)."""
-    codec.set_decoder(decoder)
-    # the shipped kernel pairs for skewed lengths
-    codec.set_encoder({"windows": "windows", "waves": "waves", "sorted": "fused"}[decoder])
+    codec.set_decoder(decoder if decoder != "region" else "sorted")
+    # the shipped kernel pairs for skewed lengths ("region": the region codes
+    # pass over the Zipf shard's packed strings, the sorted decoder)
+    codec.set_encoder({"windows": "windows", "waves": "waves", "sorted": "fused",
+                       "region": "region"}[decoder])
     try:
         _config5_rank_shard(codec, digests)
     finally:
@@ -1111,7 +1114,7 @@ def test_zipf_lengths_roundtrip(codec, alphabet):
 # the window and fused encoders per batch on the device (QH_ENCODER_AUTO:
 # the text cases here take the window path, Zipf, mixed and binary the
 # fused one).
-ENCODERS = ["windows", "waves", "fused", "auto"]
+ENCODERS = ["windows", "waves", "fused", "auto", "region"]
 
 
 @pytest.mark.parametrize("kind", ENCODERS)
