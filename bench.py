@@ -355,6 +355,7 @@ def main():
     codec.enable_timing(False)
     t_dec = timed(lambda: codec.decode_dev(enc, eout, dec, dout), args.steps)
     t_enc = timed(lambda: codec.encode_dev(src, spans, enc, eout), args.steps)
+    cold = None if args.no_configs else leg_cold(torch, codec, src, spans, enc, eout, dec, dout, total, dev)
     # packed device output (QH_WHERE_DEVICE_DENSE: the slot decode, then a
     # packing pass), reported beside the slot layout
     t_dense = timed(lambda: codec.decode_dev(enc, eout, dec, dout, dense=True), args.steps)
@@ -594,6 +595,9 @@ def main():
                       "encode_GiBps": round(total_all / t_enc / GIB, 2),
                       "decode_dense_GiBps": round(total_all / t_dense / GIB, 2),
                       "decode_dense_bit_exact": dense_ok,
+                      "decode_cold_GiBps": cold and cold["decode_cold_GiBps"],
+                      "encode_cold_GiBps": cold and cold["encode_cold_GiBps"],
+                      "cold_input": cold,
                       "two_batches_in_flight": two_ctx,
                       "enc_global_offset_rank0": enc_global_off,
                       "kernels": kern, "host_path": host_path, "counters": counters,
@@ -603,6 +607,42 @@ def main():
         }
         print(json.dumps(line), flush=True)
     D.close()
+
+
+def leg_cold(torch, codec, src, spans, enc, eout, dec, dout, total, dev, reps=9):
+    """The decoder and the encoder on a cold input: in
+    deployment the decoder's input arrives by H2D from a QUIC stream buffer,
+    not from an encoder that just wrote it on the same GPU.  Before each
+    timed call a 1 GiB scrub buffer is read and written (4x the 256 MiB
+    Infinity Cache, 32x the 8 x 4 MiB L2), outside the timed region; HIP
+    events on the codec's stream bracket the one call.  The same per-call
+    measurement without the scrub is reported beside it (warm: the round
+    trip's situation, the encoded bytes still cached from the encode)."""
+    scrub = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def one(fn, cold):
+        if cold:
+            scrub.add_(1)
+        ev[0].record()
+        fn()
+        ev[1].record()
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) * 1e-3
+
+    out = {}
+    for name, fn in (("decode", lambda: codec.decode_dev(enc, eout, dec, dout)),
+                     ("encode", lambda: codec.encode_dev(src, spans, enc, eout))):
+        fn()  # (a warm-up call, and the encoder's AUTO history)
+        ts = {c: sorted(one(fn, c) for _ in range(reps)) for c in (False, True)}
+        out[name + "_cold_GiBps"] = round(total / ts[True][reps // 2] / GIB, 2)
+        out[name + "_warm_GiBps_same_method"] = round(total / ts[False][reps // 2] / GIB, 2)
+        out[name + "_cold_us"] = round(ts[True][reps // 2] * 1e6, 1)
+        out[name + "_warm_us"] = round(ts[False][reps // 2] * 1e6, 1)
+    out["how"] = ("median of %d single calls, HIP events on the codec stream; cold: a 1 GiB "
+                  "read+write scrub before each call, outside the events" % reps)
+    del scrub
+    return out
 
 
 def leg_config4(args, torch, dev, codec, D, rank, world, timed):
@@ -805,10 +845,14 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
     d_out = torch.empty(out_bytes, dtype=torch.uint8, device=dev)
     s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
-    def probe(h2d, d2h, reps=3):
-        torch.cuda.synchronize()
-        a = time.perf_counter()
+    def probe(h2d, d2h, reps=5):
+        """The fastest of reps single transfers (the copy engines' best for
+        these byte counts: an enqueue that blocks the host until its copy is
+        done serialises the two directions in some reps)."""
+        ts = []
         for _ in range(reps):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
             if h2d:
                 with torch.cuda.stream(s1):
                     d_in.copy_(h_in, non_blocking=True)
@@ -816,7 +860,8 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
                 with torch.cuda.stream(s2):
                     h_out.copy_(d_out, non_blocking=True)
             torch.cuda.synchronize()
-        return (time.perf_counter() - a) / reps
+            ts.append(time.perf_counter() - a)
+        return min(ts)
 
     probe(True, True, 1)
     t_h2d, t_d2h, t_both = probe(True, False), probe(False, True), probe(True, True)
@@ -835,17 +880,25 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
         d_t = torch.empty(max(cap_h, 1), dtype=torch.uint8, pin_memory=pin)
         o_t = torch.empty(n * 2, dtype=torch.int64, pin_memory=pin)
         e_h, d_h, o_h = e_t.numpy(), d_t.numpy(), o_t.numpy().view(q.SPAN_OUT_DTYPE)
-        codec.decode_host(e_h, spn, d_h, o_h)  # warm the staging buffers
-        # (the median of 5 calls: the first calls after the warm one run up
-        # to twice as long on some boxes)
+        for _ in range(2):  # warm the staging buffers and the host pages
+            codec.decode_host(e_h, spn, d_h, o_h)
+        # the median of 5 calls; Python's garbage collector held off while
+        # they run (a collection inside a call is the harness's pause, not
+        # the library's)
         reps = 5
 
         def med_ms(fn):
+            import gc
             ts = []
-            for _ in range(reps):
-                a = time.perf_counter()
-                fn()
-                ts.append(time.perf_counter() - a)
+            gc.collect()
+            gc.disable()
+            try:
+                for _ in range(reps):
+                    a = time.perf_counter()
+                    fn()
+                    ts.append(time.perf_counter() - a)
+            finally:
+                gc.enable()
             return sorted(ts)[reps // 2], [round(t * 1e3, 2) for t in ts]
 
         t_host, ts_host = med_ms(lambda: codec.decode_host(e_h, spn, d_h, o_h))

@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <condition_variable>
 #include <atomic>
 #include <thread>
 #include <string>
