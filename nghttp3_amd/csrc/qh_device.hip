@@ -67,7 +67,7 @@
 #include "qh_lane_enc.inc"   // encoder: lengths (stream, lanes), codes (lanes: the default)
 #include "qh_enc_waves.inc"   // encoder codes (QH_ENCODER_WAVES): per-wave chunks, LDS rings
 #include "qh_enc_fused.inc"   // encoder, lengths + codes in one pass (QH_ENCODER_FUSED)
-#include "qh_enc_region.inc"  // encoder codes over each window's region (QH_ENCODER_REGION, AUTO for text)
+#include "qh_enc_region.inc"  // encoder codes over each window's region (QH_ENCODER_REGION, opt-in)
 #ifdef QH_DEV_VARIANTS
 #include "qh_enc_seg.inc"    // (dev/csrc) encoder, one pass over equal-size segments per lane
 #include "qh_enc_stream.inc" // encoder codes: streaming region rounds
