@@ -889,21 +889,27 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
 
         def med_ms(fn):
             import gc
-            ts = []
+            ts, thr = [], []
             gc.collect()
             gc.disable()
             try:
                 for _ in range(reps):
+                    t0 = _cpu_throttled_ms()
                     a = time.perf_counter()
                     fn()
                     ts.append(time.perf_counter() - a)
+                    t1 = _cpu_throttled_ms()
+                    thr.append(round(t1 - t0, 2) if t0 is not None and t1 is not None else None)
             finally:
                 gc.enable()
-            return sorted(ts)[reps // 2], [round(t * 1e3, 2) for t in ts]
+            return sorted(ts)[reps // 2], [round(t * 1e3, 2) for t in ts], thr
 
-        t_host, ts_host = med_ms(lambda: codec.decode_host(e_h, spn, d_h, o_h))
+        t_host, ts_host, thr_host = med_ms(lambda: codec.decode_host(e_h, spn, d_h, o_h))
+        # (cpu_throttled_ms_each: time the cgroup's CPU quota held the
+        # process's threads back during each call)
         out[kind] = {"decode_GiBps_incl_h2d_d2h": round(total / t_host / GIB, 2),
-                     "ms": round(t_host * 1e3, 2), "ms_each": ts_host}
+                     "ms": round(t_host * 1e3, 2), "ms_each": ts_host,
+                     "cpu_throttled_ms_each": thr_host}
         if pin:
             out[kind]["page_node"] = [_page_node(e_t), _page_node(d_t)]
             # the bound: both directions at once, the probe's time for these bytes
@@ -914,7 +920,7 @@ def leg_host_path(torch, codec, q, enc, eout, enc_bytes, total, n, dev):
             from nghttp3_amd import HuffmanBatchCodec
             cs = [HuffmanBatchCodec(dev.index or 0, stream=torch.cuda.Stream(dev)) for _ in range(2)]
             HuffmanBatchCodec.decode_host_multi(cs, e_h, spn, d_h, o_h)  # warm
-            t_m, ts_m = med_ms(lambda: HuffmanBatchCodec.decode_host_multi(cs, e_h, spn, d_h, o_h))
+            t_m, ts_m, _ = med_ms(lambda: HuffmanBatchCodec.decode_host_multi(cs, e_h, spn, d_h, o_h))
             out["pinned_2ctx_one_gpu"] = {"decode_GiBps_incl_h2d_d2h": round(total / t_m / GIB, 2),
                                           "ms": round(t_m * 1e3, 2), "ms_each": ts_m,
                                           "frac_of_probe_both": round(t_both / t_m, 3)}
@@ -980,10 +986,8 @@ def leg_host_path_ranks(torch, codec, q, src, enc, eout, enc_bytes, total, n, de
     return out
 
 
-def _cpu_quota():
-    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max
-    or v1 cfs quota / period), rounded up; None when unlimited / unknown."""
-    import math
+def _cg_paths():
+    """This process's cgroup directories that may hold its CPU controller."""
     paths = []
     try:
         for line in open("/proc/self/cgroup"):
@@ -997,7 +1001,30 @@ def _cpu_quota():
     except OSError:
         pass
     paths += [("v2", "/sys/fs/cgroup"), ("v1", "/sys/fs/cgroup/cpu"), ("v1", "/sys/fs/cgroup/cpu,cpuacct")]
-    for kind, d in paths:
+    return paths
+
+
+def _cpu_throttled_ms():
+    """Milliseconds the cgroup's CPU quota has held this process's threads
+    back so far (cpu.stat throttled_usec / throttled_time); None if unknown."""
+    for kind, d in _cg_paths():
+        try:
+            for line in open(os.path.join(d, "cpu.stat")):
+                k, v = line.split()[:2]
+                if k == "throttled_usec":
+                    return int(v) / 1e3
+                if k == "throttled_time":  # (v1: ns)
+                    return int(v) / 1e6
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+def _cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max
+    or v1 cfs quota / period), rounded up; None when unlimited / unknown."""
+    import math
+    for kind, d in _cg_paths():
         try:
             if kind == "v2":
                 q, per = open(os.path.join(d, "cpu.max")).read().split()[:2]

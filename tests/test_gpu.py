@@ -438,6 +438,51 @@ def test_host_path_multi_device(codec, digests):
             c.close()
 
 
+def test_host_path_from_fresh_threads(codec, digests):
+    """The host path's returner thread makes the context's device current
+    itself (hipSetDevice(c->device) in decode_host_impl): decode_host called
+    from a Python thread that never touched the GPU, and
+    qh_decode_batch_multi over one context from another, both give the
+    plaintext back -- the single-GPU run of the paths
+    test_host_path_multi_device covers on a multi-GPU node."""
+    import threading
+    torch = torch_mod()
+    from nghttp3_amd import HuffmanBatchCodec
+    d = digests["c3_A"]
+    n = 1 << 18  # two slices' worth and more (kHostSliceMin = 2^17)
+    src, spans, total = codec.synth(d["seed"], n, d["lo"], d["hi"], synth.ALPHABET_A)
+    ln = spans[:, 1] & 0xFFFFFFFF
+    enc = torch.zeros(int(((ln * 30 + 7) // 8).sum().item()), dtype=torch.uint8, device="cuda")
+    eout = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    codec.encode_dev(src, spans, enc, eout)
+    torch.cuda.synchronize()
+    eo = eout.cpu().numpy()
+    sp = np.zeros(n, dtype=q.SPAN_IN_DTYPE)
+    sp["off"], sp["len"] = eo[:, 0], eo[:, 1] & 0xFFFFFFFF
+    e_h = enc[:int(sp["len"].sum())].cpu().numpy()
+    plain = src[:total].cpu().numpy()
+    lens = ln.cpu().numpy()
+    res = {}
+
+    def single():
+        res["single"] = codec.decode_host(e_h, sp)
+
+    def multi():
+        res["multi"] = HuffmanBatchCodec.decode_host_multi([codec], e_h, sp)
+
+    for fn in (single, multi):
+        t = threading.Thread(target=fn)
+        t.start()
+        t.join(timeout=120)
+        assert not t.is_alive()
+    for key in ("single", "multi"):
+        dst, out = res[key]
+        assert (out["status"] == 0).all() and (out["len"] == lens).all(), key
+        got = np.concatenate([dst[o:o + n_] for o, n_ in
+                              zip(out["off"].astype(np.int64), lens.astype(np.int64))])
+        assert got.tobytes() == plain.tobytes(), key
+
+
 def test_host_path_multi_refuses_a_context_twice(codec, corpus):
     """One thread per context: the same context twice in the list is refused
     (QH_ERR_INVALID_ARGUMENT) before any work starts."""
