@@ -13,5 +13,5 @@ for L in "$@"; do
 import json;d=json.loads(open('$O/b$i.json').read().strip().splitlines()[-1])
 k=d['extra']['kernels']; r=d['roofline']; e=d['extra']
 print('$L', d['value'], d['ms_per_step'], {n: v['avg_us'] for n,v in k.items()}, r.get('traffic'),
-      {x: e.get(x) for x in ('encode_GiBps','decode_GiBps','encode_cold_GiBps','decode_cold_GiBps')})"
+      {x: e.get(x) for x in ('encode_GiBps','decode_GiBps','decode_dense_GiBps','encode_cold_GiBps','decode_cold_GiBps')})"
 done
