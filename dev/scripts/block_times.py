@@ -43,7 +43,8 @@ def main():
     t0 = a[:, 0].min()
     st = (a[:, 0] - t0) / 100.0
     life = a[:, 1] / 100.0
-    hw = a[:, 2]
+    hw = a[:, 2] & 0xFFFFFFFF
+    xcd = (a[:, 2] >> 32) & 7  # (XCC_ID, recorded by the stamps build since round 6)
     # HW_ID (gfx9): wave 3:0, simd 5:4, pipe 7:6, cu 11:8, sh 12, se 15:13
     cu = (hw >> 8) & 15
     se = (hw >> 13) & 7
@@ -56,7 +57,9 @@ def main():
     mhz = a[:, 3] / np.maximum(a[:, 1], 1) * 100.0
     print("  clock MHz by blockIdx%8: " + "  ".join(
         f"{k}:{np.mean(mhz[bx % 8 == k]):.0f}" for k in range(8)))
-    for name, key in (("blockIdx%8", bx % 8), ("se", se), ("sh", sh)):
+    print("  clock MHz by xcd: " + "  ".join(f"{k}:{np.mean(mhz[xcd == k]):.0f}" for k in range(8)))
+    print("  blockIdx%8 == xcd for", int((bx % 8 == xcd).sum()), "of", len(a), "blocks")
+    for name, key in (("xcd", xcd), ("blockIdx%8", bx % 8), ("se", se), ("sh", sh)):
         g = defaultdict(list)
         for k, v in zip(key, life):
             g[int(k)].append(v)

@@ -73,7 +73,9 @@ struct StampAcc {
       if (blockIdx.x < 8192) {
         g_blk[blockIdx.x][0] = r0;
         g_blk[blockIdx.x][1] = life;
-        g_blk[blockIdx.x][2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        // HW_ID, and the XCD (XCC_ID) in bits 32..34
+        g_blk[blockIdx.x][2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                               (unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u) << 32;
         g_blk[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - t0;
       }
     }
