@@ -1279,6 +1279,21 @@ def test_cu_masked_stream_fallbacks(corpus):
                         b["lines"][:nl * 24].cpu().numpy().tobytes(), b["verdict"][:ns].cpu().numpy().tobytes(),
                         b["status"][:20000].cpu().numpy().tobytes(), ns, nl))
         assert got[0][5] > 0 and got[0] == got[1]
+        # the host-memory decode: on the full-chip context its pipeline runs
+        # on the context's own streams, on the CU-masked one it stays on the
+        # caller's stream (decode_host_impl); both give the corpus back
+        enc, eoff, elen = corpus["enc"], corpus["enc_off"], corpus["enc_len"]
+        sp_h = np.zeros(len(elen), dtype=q.SPAN_IN_DTYPE)
+        sp_h["off"], sp_h["len"] = eoff, elen
+        outs = []
+        for c in (full, part):
+            dst_h, out_h = c.decode_host(enc, sp_h)
+            assert (out_h["status"] == 0).all() and (out_h["len"] == corpus["len"]).all()
+            outs.append(b"".join(dst_h[o:o + n_].tobytes() for o, n_ in
+                                 zip(out_h["off"].astype(np.int64), out_h["len"].astype(np.int64))))
+        want = b"".join(corpus["plain"][o:o + n_].tobytes() for o, n_ in
+                        zip(corpus["off"].astype(np.int64), corpus["len"].astype(np.int64)))
+        assert outs[0] == outs[1] == want
     finally:
         part.close()
         full.close()
